@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + ms/frame, 3840x2160 Cornell box, 8 spp path trace (BASELINE.json).
+
+One *step* = one full 8-spp render of the workload: KernelEntry launched for frames
+1..8 (9 light bounces, the reference defaults) into one accumulation buffer, then -- for
+N > 1 -- the per-rank row tiles gathered to rank 0 over RCCL (torch.distributed "nccl").
+Scene and output stay resident in HBM; nothing is read back to the host inside the
+timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Rays are counted as the reference's Intersect() calls over all bounces and frames
+(SURVEY.md 8(d)); the count comes from an instrumented pass before the timed region and
+is deterministic (the HIP path is bit-exact with the oracle, tests/test_gpu_parity.py).
+
+Roofline: the dominant kernel is KernelEntry.  achieved = algorithmic bytes per launch
+(48*node_visits + 48*tri_tests + 164*hits + 32*W*H) / average launch
+duration from HIP events recorded on the kernel's own stream during the timed region;
+peak = 8000 GB/s (MI355X HBM3E).  traffic = HBM bytes per launch from rocprofv3 PMC
+counters (profiles/traffic.json, written by scripts/profile.sh) when present.
+cpu_baseline: the CPU oracle (a C restatement of kernel_bvh.cl) on the host cores, rank 0,
+N = 1 only, on a bounded sample (frames 1-2 of the same 4K render).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mini-opencl-raytracer_amd"))
+
+import clrt  # noqa: E402
+from clrt import _native as N  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--width", type=int, default=3840)
+    p.add_argument("--height", type=int, default=2160)
+    p.add_argument("--frames", type=int, default=8)
+    p.add_argument("--bounces", type=int, default=9)
+    p.add_argument("--math", choices=["pinned", "devicelib"], default="pinned")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+class Rank:
+    """One GPU's share of the image: rows [row0, row1) as work-items [row0*W, row1*W)."""
+
+    def __init__(self, scene, args, device, rank, world):
+        self.args = args
+        W, H = args.width, args.height
+        self.W, self.H = W, H
+        rows = (H + world - 1) // world
+        self.rows_per_rank = rows
+        self.row0 = min(H, rank * rows)
+        self.row1 = min(H, self.row0 + rows)
+        self.ctx = clrt.CLContext(device)
+        self.k = clrt.CLKernel(self.ctx, "KernelEntry")
+        flags = N.MEM_READ_ONLY | N.MEM_COPY_HOST_PTR
+        self.bufs = [self.ctx.create_buffer(flags, a.nbytes, a)
+                     for a in (scene.triangles, scene.nodes, scene.materials)]
+        self.out = self.ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+        k = self.k
+        k.set_buffer(N.BUFFER_OUT, self.out)
+        k.set_buffer(N.BUFFER_SCENE, self.bufs[0])
+        k.set_buffer(N.BUFFER_NODE, self.bufs[1])
+        k.set_buffer(N.BUFFER_MATERIAL, self.bufs[2])
+        k.set_int(N.WIDTH, W)
+        k.set_int(N.HEIGHT, H)
+        k.set_uint(N.FRAME_SEED, 0)
+        k.set_int(N.LIGHT_BOUNCES, args.bounces)
+        k.set_int(N.LIGHT_TYPE, 0)
+        k.set_float(N.SKYBOX_INTENSITY, 1.0)
+        k.set_float3(N.CAMERA_POS, CAMERA[0])
+        k.set_float3(N.CAMERA_FRONT, CAMERA[1])
+        k.set_float3(N.CAMERA_UP, CAMERA[2])
+        k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
+        k.set_work_range(self.row0 * W, self.row1 * W)
+
+    def render(self):
+        """frames 1..F accumulated (RenderFrame's m_FrameCount sequence)."""
+        for f in range(1, self.args.frames + 1):
+            self.k.set_uint(N.FRAME_COUNT, f)
+            self.ctx.ExecuteKernel(self.k, self.W * self.H)
+
+    def finish(self):
+        self.ctx.Finish()
+
+
+def count_pass(r):
+    r.k.set_stats(True)
+    r.k.reset_stats()
+    r.render()
+    r.finish()
+    s = r.k.stats()
+    r.k.set_stats(False)
+    r.k.reset_stats()
+    return s
+
+
+def cpu_baseline(scene, args):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    W, H = args.width, args.height
+    threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+    res = np.zeros((W * H, 4), np.float32)
+    rays = 0
+    t0 = time.perf_counter()
+    sample_frames = 2
+    for f in range(1, sample_frames + 1):
+        res, _, _, c = oracle.render(scene, W, H, frame_count=f, light_bounces=args.bounces, result=res,
+                                     threads=threads)
+        rays += c["rays"]
+    dt = time.perf_counter() - t0
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"frames 1-{sample_frames} of the same {W}x{H} {args.bounces}-bounce render, all pixels "
+                      f"({rays} rays, {dt:.2f} s wall)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+
+    scene = clrt.scene.cornell()
+    r = Rank(scene, args, local, rank, world)
+
+    # instrumented pass: ray / node / triangle / hit counts of one step on this rank
+    st = count_pass(r)
+    counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
+
+    gather = None
+    if dist is not None:
+        import torch
+        tile_bytes = r.rows_per_rank * r.W * 16
+        tile = torch.empty(tile_bytes // 4, dtype=torch.float32, device=f"cuda:{local}")
+        full = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
+
+        def gather():
+            # this rank's rows -> staging tensor (device to device on the kernel's stream),
+            # then gather of the row tiles to rank 0 over RCCL (grouped send/recv)
+            n = (r.row1 - r.row0) * r.W * 16
+            if n:
+                r.ctx.CopyToDevicePointer(r.out, r.row0 * r.W * 16, n, tile.data_ptr())
+                r.finish()
+            dist.gather(tile, full, dst=0)
+
+        tot = torch.tensor(counts, dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tot)
+        counts = tot.cpu().numpy()
+
+    def step():
+        r.render()
+        r.finish()
+        if gather is not None:
+            gather()
+
+    for _ in range(args.warmup):
+        step()
+
+    def sync_all():
+        r.finish()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    r.k.set_timing(True)
+    r.k.reset_stats()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    ks = r.k.stats()
+    r.k.set_timing(False)
+    if dist is not None:
+        import torch
+        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    rays_per_step, visits, tests, hits = counts
+    ms_step = elapsed * 1e3 / args.steps
+    value = rays_per_step * args.steps / elapsed / 1e6
+    # roofline of KernelEntry on rank 0: algorithmic bytes of one launch (one frame of this
+    # rank's tile) / its mean duration
+    launches = max(1, ks["launches"])
+    kernel_ms = ks["kernel_ms"] / launches
+    local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
+    tile_px = (r.row1 - r.row0) * r.W
+    alg_bytes = (48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames + 32 * tile_px
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            key = f"{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except (ValueError, KeyError):
+            traffic = None
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    line = {
+        "metric": "Mrays/s (3840x2160 Cornell box, 8 spp, 9 bounces)",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "ms_per_frame": round(ms_step / args.frames, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "reference scene cornell.obj (scenes/cornell_scene.npz); rays generated in-kernel",
+        "config": {"workload": f"cornell {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
+                   "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
+                   "math": args.math, "parallelism": f"row tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
+                   "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
+                     "alg_bytes_per_launch": int(alg_bytes)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(scene, args)
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X hot path (librt_hip.so).
+ *
+ * Drop-in for the reference's OpenCL device boundary: the CLContext / CLKernel wrapper
+ * (/root/reference/CLutils.h:107-145, CLutils.cpp:9-77) and the clCreateBuffer calls of
+ * its callers (CLBVHnode.cpp:209-236, CLRaytracer.cpp:122-137).  Plain C types only;
+ * every entry point returns 0 (RT_SUCCESS) or a negative cl_int-style code from
+ * rt_status.h -- no exception crosses the ABI (the C++ wrapper in rt_cl_compat.hpp
+ * turns codes back into the reference's CLException).
+ *
+ * The kernel "KernelEntry" is precompiled for gfx950 (no runtime JIT).  It takes the
+ * reference's 14 argument slots (RenderKernelArgument_t, CLutils.h:11-27):
+ *    0 BUFFER_OUT (rt_mem)       4 WIDTH (uint)        8 LIGHT_BOUNCES (int)
+ *    1 BUFFER_SCENE (rt_mem)     5 HEIGHT (uint)       9 LIGHT_TYPE (int)
+ *    2 BUFFER_NODE (rt_mem)      6 FRAME_COUNT (uint) 10 SKYBOX_INTENSITY (float)
+ *    3 BUFFER_MATERIAL (rt_mem)  7 FRAME_SEED (uint)  11-13 CAMERA_POS/FRONT/UP (float3,
+ *                                                        16 bytes, w ignored)
+ * Buffers hold the CLTriangle / CLLinearBVHNode / CLMaterial bytes of rt_cl_types.h;
+ * the output is one 16-byte float3 slot per work-item, as the reference's.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_context_s* rt_context; /* cl::Context + in-order cl::CommandQueue */
+typedef struct rt_mem_s* rt_mem;         /* cl::Buffer */
+typedef struct rt_kernel_s* rt_kernel;   /* cl::Kernel */
+
+/* cl_mem_flags values (CL/cl.h) accepted by rtCreateBuffer */
+#define RT_MEM_READ_WRITE (1u << 0)
+#define RT_MEM_WRITE_ONLY (1u << 1)
+#define RT_MEM_READ_ONLY (1u << 2)
+#define RT_MEM_COPY_HOST_PTR (1u << 5)
+
+/* RenderKernelArgument_t (CLutils.h:11-27) */
+enum rt_kernel_arg {
+    RT_ARG_BUFFER_OUT = 0,
+    RT_ARG_BUFFER_SCENE = 1,
+    RT_ARG_BUFFER_NODE = 2,
+    RT_ARG_BUFFER_MATERIAL = 3,
+    RT_ARG_WIDTH = 4,
+    RT_ARG_HEIGHT = 5,
+    RT_ARG_FRAME_COUNT = 6,
+    RT_ARG_FRAME_SEED = 7,
+    RT_ARG_LIGHT_BOUNCES = 8,
+    RT_ARG_LIGHT_TYPE = 9,
+    RT_ARG_SKYBOX_INTENSITY = 10,
+    RT_ARG_CAMERA_POS = 11,
+    RT_ARG_CAMERA_FRONT = 12,
+    RT_ARG_CAMERA_UP = 13,
+    RT_ARG_COUNT = 14
+};
+
+/* ---- reference surface --------------------------------------------------------------- */
+
+/* CLContext::CLContext(platform) (CLutils.cpp:9-35): context + in-order queue on GPU
+ * `device_index` (the reference always takes device[0]). */
+int rtCreateContext(int device_index, rt_context* out);
+int rtReleaseContext(rt_context ctx);
+
+/* cl::Buffer(context, flags, size, host_ptr) (CLBVHnode.cpp:215-236,
+ * CLRaytracer.cpp:132-135).  With RT_MEM_COPY_HOST_PTR the device gets a copy of
+ * `size` bytes of `host_ptr` and the caller keeps its memory.  Other buffers are
+ * zero-filled (the reference leaves the output buffer uninitialised). */
+int rtCreateBuffer(rt_context ctx, uint64_t flags, size_t size, const void* host_ptr, rt_mem* out);
+int rtReleaseBuffer(rt_mem mem);
+
+/* CLKernel::CLKernel(file, devices) (CLutils.cpp:52-66).  The only kernel name is
+ * "KernelEntry"; any other -> RT_INVALID_KERNEL_NAME. */
+int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out);
+int rtReleaseKernel(rt_kernel k);
+
+/* CLKernel::SetArgument(index, data, size) (CLutils.cpp:68-77).  Buffer slots take a
+ * pointer to an rt_mem and size == sizeof(rt_mem); scalar slots size 4; float3 slots
+ * size 16 (the reference's host float3, CLmathlib.hpp:18-54).  Values are copied;
+ * they persist across launches (set-then-launch, as in RenderFrame). */
+int rtSetKernelArg(rt_kernel k, unsigned index, size_t size, const void* value);
+
+/* CLContext::ExecuteKernel(kernel, workSize) (CLutils.cpp:44-50): one work-item per
+ * pixel, 1-D NDRange of `global_work_size` (= width*height in the reference).
+ * Asynchronous on the context's in-order stream. */
+int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size);
+
+/* CLContext::ReadBuffer (CLutils.cpp:37-42, non-blocking in the reference) and
+ * CLContext::Finish (CLutils.h:122-125). */
+int rtEnqueueReadBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset, size_t size,
+                        void* dst);
+int rtFinish(rt_context ctx);
+
+/* ---- extensions (no reference counterpart) ------------------------------------------- */
+
+int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset, size_t size,
+                         const void* src);
+
+/* Math policy of the kernel: RT_MATH_PINNED (default; bit-identical to the pinned CPU
+ * semantics of rt_pinned_math.h) or RT_MATH_DEVICELIB (the AMD OpenCL device-library
+ * builtins the reference kernel gets on this GPU). */
+#define RT_MATH_PINNED 0
+#define RT_MATH_DEVICELIB 1
+int rtKernelSetMathMode(rt_kernel k, int mode);
+
+/* Restrict the next launches to work-items [first, last) (pixel-row tiles for
+ * multi-GPU sharding); last = 0 means "to global_work_size".  Work-item ids, and
+ * therefore seeds and output slots, stay global. */
+int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last);
+
+/* Primary-ray outputs per work-item: hit primitive index into the BVH-ordered triangle
+ * array (-1 = miss) and isect.t.  Pass NULL to disable. Buffers need 4 B per work-item. */
+int rtKernelSetHitBuffers(rt_kernel k, rt_mem hit_ids, rt_mem hit_t);
+
+/* Counters (section 8(d) of SURVEY.md): rays = Intersect() calls, node visits,
+ * triangle tests, closest hits.  Enabling selects an instrumented kernel variant. */
+typedef struct rt_stats {
+    uint64_t rays, node_visits, tri_tests, hits;
+    uint64_t launches;
+    double kernel_ms;  /* sum of KernelEntry durations (HIP events) when timing is on */
+} rt_stats;
+int rtKernelSetStats(rt_kernel k, int enable);
+int rtKernelSetTiming(rt_kernel k, int enable);
+int rtKernelGetStats(rt_kernel k, rt_stats* out);
+int rtKernelResetStats(rt_kernel k);
+
+/* Where the scene lives: 1 = staged in LDS (when it fits), 0 = read from HBM/L2. */
+int rtKernelGetSceneInLDS(rt_kernel k, int* in_lds);
+/* Force the global-memory path even if the scene fits in LDS (testing). */
+int rtKernelForceGlobalScene(rt_kernel k, int force);
+
+/* Device-to-device copy of [offset, offset+size) of `src` to a device address (e.g. a
+ * collective's staging tensor), asynchronous on the context's stream. */
+int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem src, size_t offset, size_t size, void* dst_device);
+
+/* Device address of a buffer and the context's HIP stream (for collectives/interop). */
+int rtBufferGetDevicePointer(rt_mem mem, void** dptr);
+int rtBufferGetSize(rt_mem mem, size_t* size);
+int rtContextGetStream(rt_context ctx, void** hip_stream);
+int rtContextGetDevice(rt_context ctx, int* device_index);
+
+/* Library identification (for smoke checks): returns a static string. */
+const char* rtGetBuildInfo(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */

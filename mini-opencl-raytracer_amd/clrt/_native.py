@@ -1,0 +1,150 @@
+"""ctypes bindings of the two product libraries (include/rt_hip.h, include/rt_scene.h).
+
+The libraries are built in-tree by ``make -C mini-opencl-raytracer_amd`` (or
+``__graft_entry__.build()``).  Nothing here falls back to a CPU path: if
+``librt_hip.so`` is missing or no GPU is visible, the calls fail with ``RTError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(_PKG_ROOT, "lib")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "librt_hip.so")
+SCENE_LIB_PATH = os.path.join(LIB_DIR, "librt_scene.so")
+
+# ---- status codes (include/rt_status.h == cl_int codes, CLutils.h:31-105) -------------
+RT_SUCCESS = 0
+_ERROR_NAMES = {
+    0: "CL_SUCCESS", -1: "CL_DEVICE_NOT_FOUND", -4: "CL_MEM_OBJECT_ALLOCATION_FAILURE",
+    -5: "CL_OUT_OF_RESOURCES", -6: "CL_OUT_OF_HOST_MEMORY", -30: "CL_INVALID_VALUE",
+    -33: "CL_INVALID_DEVICE", -34: "CL_INVALID_CONTEXT", -36: "CL_INVALID_COMMAND_QUEUE",
+    -37: "CL_INVALID_HOST_PTR", -38: "CL_INVALID_MEM_OBJECT", -46: "CL_INVALID_KERNEL_NAME",
+    -48: "CL_INVALID_KERNEL", -49: "CL_INVALID_ARG_INDEX", -50: "CL_INVALID_ARG_VALUE",
+    -51: "CL_INVALID_ARG_SIZE", -52: "CL_INVALID_KERNEL_ARGS", -59: "CL_INVALID_OPERATION",
+    -61: "CL_INVALID_BUFFER_SIZE", -63: "CL_INVALID_GLOBAL_WORK_SIZE",
+    -1001: "RT_FILE_NOT_FOUND", -1002: "RT_PARSE_ERROR",
+}
+
+
+def error_string(code: int) -> str:
+    """GetClErrorString (CLutils.h:31-105)."""
+    return _ERROR_NAMES.get(int(code), "Unknown OpenCL error")
+
+
+class RTError(RuntimeError):
+    """CLException (CLutils.h:107-114): ``message (CL_NAME)`` plus the numeric code."""
+
+    def __init__(self, message: str, code: int):
+        super().__init__(f"{message} ({error_string(code)})")
+        self.code = int(code)
+
+
+def check(code: int, message: str) -> None:
+    if code != RT_SUCCESS:
+        raise RTError(message, code)
+
+
+# ---- rt_cl_types.h as numpy dtypes ------------------------------------------------------
+FLOAT3 = np.dtype((np.float32, 4))  # OpenCL float3: 16-byte slot
+VERTEX_DTYPE = np.dtype([("position", FLOAT3), ("uv", FLOAT3), ("normal", FLOAT3),
+                         ("tangent_s", FLOAT3), ("tangent_t", FLOAT3)])
+TRIANGLE_DTYPE = np.dtype([("v1", VERTEX_DTYPE), ("v2", VERTEX_DTYPE), ("v3", VERTEX_DTYPE),
+                           ("mtlIndex", np.uint32), ("padding", np.uint32, (3,))])
+NODE_DTYPE = np.dtype([("bmin", FLOAT3), ("bmax", FLOAT3), ("offset", np.uint32),
+                       ("nPrimitives", np.uint16), ("axis", np.uint8), ("pad", np.uint8, (9,))])
+MATERIAL_DTYPE = np.dtype([("diffuse", FLOAT3), ("specular", FLOAT3), ("emission", FLOAT3),
+                           ("type", np.uint32), ("roughness", np.float32), ("ior", np.float32),
+                           ("padding", np.int32)])
+assert VERTEX_DTYPE.itemsize == 80 and TRIANGLE_DTYPE.itemsize == 256
+assert NODE_DTYPE.itemsize == 48 and MATERIAL_DTYPE.itemsize == 64
+
+# RenderKernelArgument_t (CLutils.h:11-27)
+BUFFER_OUT, BUFFER_SCENE, BUFFER_NODE, BUFFER_MATERIAL = 0, 1, 2, 3
+WIDTH, HEIGHT, FRAME_COUNT, FRAME_SEED = 4, 5, 6, 7
+LIGHT_BOUNCES, LIGHT_TYPE, SKYBOX_INTENSITY = 8, 9, 10
+CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
+
+MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
+MATH_PINNED, MATH_DEVICELIB = 0, 1
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
+                ("tri_tests", ctypes.c_uint64), ("hits", ctypes.c_uint64),
+                ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
+
+
+_vp = ctypes.c_void_p
+_HIP_PROTOS = {
+    "rtCreateContext": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rtReleaseContext": (ctypes.c_int, [_vp]),
+    "rtCreateBuffer": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_size_t, _vp, ctypes.POINTER(_vp)]),
+    "rtReleaseBuffer": (ctypes.c_int, [_vp]),
+    "rtCreateKernel": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "rtReleaseKernel": (ctypes.c_int, [_vp]),
+    "rtSetKernelArg": (ctypes.c_int, [_vp, ctypes.c_uint, ctypes.c_size_t, _vp]),
+    "rtEnqueueKernel": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "rtEnqueueReadBuffer": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, _vp]),
+    "rtEnqueueWriteBuffer": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, _vp]),
+    "rtFinish": (ctypes.c_int, [_vp]),
+    "rtEnqueueCopyBufferToPointer": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
+    "rtKernelSetMathMode": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtKernelSetWorkRange": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
+    "rtKernelSetHitBuffers": (ctypes.c_int, [_vp, _vp, _vp]),
+    "rtKernelSetStats": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtKernelSetTiming": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtKernelGetStats": (ctypes.c_int, [_vp, ctypes.POINTER(Stats)]),
+    "rtKernelResetStats": (ctypes.c_int, [_vp]),
+    "rtKernelGetSceneInLDS": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "rtKernelForceGlobalScene": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtBufferGetDevicePointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "rtBufferGetSize": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
+    "rtContextGetStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "rtContextGetDevice": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "rtGetBuildInfo": (ctypes.c_char_p, []),
+}
+HIP_EXPORTS = tuple(_HIP_PROTOS)
+
+_SCENE_PROTOS = {
+    "rtsLoadOBJ": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint, ctypes.POINTER(_vp)]),
+    "rtsLoadOBJUnbuilt": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "rtsBuildFromTriangles": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint,
+                                             ctypes.POINTER(_vp)]),
+    "rtsGetTriangles": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
+    "rtsGetNodes": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
+    "rtsGetMaterials": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
+    "rtsGetTreeStats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
+                                       ctypes.POINTER(ctypes.c_uint)]),
+    "rtsRelease": (None, [_vp]),
+}
+SCENE_EXPORTS = tuple(_SCENE_PROTOS)
+
+_libs: dict = {}
+
+
+def _load(path: str, protos: dict) -> ctypes.CDLL:
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RTError(f"{os.path.basename(path)} is not built (run __graft_entry__.build())", -59)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _libs[path] = lib
+    return lib
+
+
+def hip_lib() -> ctypes.CDLL:
+    """librt_hip.so -- the HIP hot path.  Loading it does not touch the GPU."""
+    return _load(HIP_LIB_PATH, _HIP_PROTOS)
+
+
+def scene_lib() -> ctypes.CDLL:
+    """librt_scene.so -- the host scene pipeline."""
+    return _load(SCENE_LIB_PATH, _SCENE_PROTOS)

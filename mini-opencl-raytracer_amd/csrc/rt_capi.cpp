@@ -1,0 +1,609 @@
+// rt_capi.cpp -- the C ABI of include/rt_hip.h over the HIP runtime.
+//
+// Objects mirror the reference's OpenCL objects one to one:
+//   rt_context = cl::Context + in-order cl::CommandQueue (CLutils.cpp:9-35) -> one HIP
+//                device + one non-blocking HIP stream;
+//   rt_mem     = cl::Buffer (CLBVHnode.cpp:215-236, CLRaytracer.cpp:132-135) -> hipMalloc
+//                allocation (+ a host shadow of what the host last wrote, used to
+//                validate scene arrays before any kernel reads them);
+//   rt_kernel  = cl::Kernel "KernelEntry" (CLutils.cpp:52-77) -> the argument slots and
+//                the derived packed scene the HIP kernels read.
+// Safety: the node/triangle/material arrays are validated on the host before the first
+// launch that uses them (child indices strictly increasing, leaf ranges inside the
+// triangle array, material indices in range, depth <= 64), so a malformed scene is an
+// error code, never an out-of-bounds or non-terminating GPU walk.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/rt_cl_types.h"
+#include "../../include/rt_hip.h"
+#include "rt_kernels.hpp"
+
+namespace {
+
+constexpr uint64_t kKnownFlags =
+    RT_MEM_READ_WRITE | RT_MEM_WRITE_ONLY | RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
+constexpr int kMaxStack = 64;                  // nodesToVisit[64], kernel_bvh.cl:181
+constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
+
+int map_hip(hipError_t e) {
+    switch (e) {
+        case hipSuccess: return RT_SUCCESS;
+        case hipErrorOutOfMemory: return RT_MEM_OBJECT_ALLOCATION_FAILURE;
+        case hipErrorNoDevice:
+        case hipErrorInvalidDevice: return RT_DEVICE_NOT_FOUND;
+        case hipErrorLaunchOutOfResources: return RT_OUT_OF_RESOURCES;
+        default: return RT_INVALID_OPERATION;
+    }
+}
+
+}  // namespace
+
+struct rt_context_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 0;
+};
+
+struct rt_mem_s {
+    rt_context ctx = nullptr;
+    void* dptr = nullptr;
+    size_t size = 0;
+    uint64_t flags = 0;
+    std::vector<uint8_t> shadow;  // host copy of the bytes (valid when shadow_valid)
+    bool shadow_valid = false;
+    uint64_t generation = 0;      // bumped on every host write
+};
+
+struct rt_kernel_s {
+    rt_context ctx = nullptr;
+    bool set[RT_ARG_COUNT] = {};
+    rt_mem bufs[4] = {};
+    uint32_t u32[RT_ARG_COUNT] = {};  // slots 4..10 (raw 4-byte values)
+    float f3[3][4] = {};              // slots 11..13
+    int math = RT_MATH_PINNED;
+    uint64_t range_first = 0, range_last = 0;
+    rt_mem hit_ids = nullptr, hit_t = nullptr;
+    bool stats = false, timing = false, force_global = false;
+    unsigned long long* dstats = nullptr;  // device counters [4]
+    uint64_t launches = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+    std::vector<hipEvent_t> event_pool;
+    double kernel_ms = 0.0;
+    // derived packed scene
+    rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
+    uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
+    float4* packed_nodes = nullptr;
+    float4* packed_tris = nullptr;
+    size_t packed_nodes_cap = 0, packed_tris_cap = 0;
+    uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
+    int depth = 0;
+    bool last_lds = false;
+    int occ_cache[2][2][2] = {};  // [math][lds][stats] -> blocks per CU (0 = unknown)
+    size_t occ_smem[2][2][2] = {};
+};
+
+namespace {
+
+int ensure_device(rt_context ctx) {
+    if (!ctx) return RT_INVALID_CONTEXT;
+    return map_hip(hipSetDevice(ctx->device));
+}
+
+// Host view of a buffer's bytes (shadow, or a device read-back).
+int host_bytes(rt_mem m, std::vector<uint8_t>& tmp, const uint8_t** out) {
+    if (m->shadow_valid) {
+        *out = m->shadow.data();
+        return RT_SUCCESS;
+    }
+    tmp.resize(m->size);
+    hipError_t e = hipMemcpyAsync(tmp.data(), m->dptr, m->size, hipMemcpyDeviceToHost, m->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(m->ctx->stream);
+    if (e != hipSuccess) return map_hip(e);
+    *out = tmp.data();
+    return RT_SUCCESS;
+}
+
+// Validate the flattened BVH (CLBVHnode.cpp:161-183 contract) and return its depth.
+int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* depth_out) {
+    if (n == 0) return RT_INVALID_MEM_OBJECT;
+    std::vector<int> depth(n, -1);
+    depth[0] = 0;
+    int max_depth = 0;
+    // children have larger indices than their parent, so one forward sweep sets depths
+    for (uint32_t i = 0; i < n; ++i) {
+        if (depth[i] < 0) continue;  // unreachable node: never visited by the kernel
+        const rt_cl_bvh_node& x = nd[i];
+        if (x.nPrimitives > 0) {
+            if ((uint64_t)x.offset + x.nPrimitives > n_tris) return RT_INVALID_MEM_OBJECT;
+            max_depth = std::max(max_depth, depth[i]);
+        } else {
+            if (x.axis > 2) return RT_INVALID_MEM_OBJECT;
+            const uint64_t a = (uint64_t)i + 1, b = x.offset;
+            if (a >= n || b >= n || b <= a) return RT_INVALID_MEM_OBJECT;
+            depth[a] = std::max(depth[a], depth[i] + 1);
+            depth[b] = std::max(depth[b], depth[i] + 1);
+        }
+    }
+    *depth_out = max_depth;
+    return max_depth > kMaxStack ? RT_INVALID_MEM_OBJECT : RT_SUCCESS;
+}
+
+int prepare_scene(rt_kernel k) {
+    rt_mem tm = k->bufs[RT_ARG_BUFFER_SCENE], nm = k->bufs[RT_ARG_BUFFER_NODE],
+           mm = k->bufs[RT_ARG_BUFFER_MATERIAL];
+    if (tm->size < sizeof(rt_cl_triangle) || nm->size < sizeof(rt_cl_bvh_node) ||
+        mm->size < sizeof(rt_cl_material))
+        return RT_INVALID_MEM_OBJECT;
+    const uint32_t nt = (uint32_t)(tm->size / sizeof(rt_cl_triangle));
+    const uint32_t nn = (uint32_t)(nm->size / sizeof(rt_cl_bvh_node));
+    const uint32_t nmat = (uint32_t)(mm->size / sizeof(rt_cl_material));
+    const bool tris_stale = k->packed_for_tris != tm || k->packed_tris_gen != tm->generation;
+    const bool nodes_stale = k->packed_for_nodes != nm || k->packed_nodes_gen != nm->generation;
+    const bool mats_stale = k->checked_mats != mm || k->checked_mats_gen != mm->generation;
+    if (!tris_stale && !nodes_stale && !mats_stale) return RT_SUCCESS;
+
+    std::vector<uint8_t> tmp_t, tmp_n;
+    const uint8_t *tb = nullptr, *nb = nullptr;
+    int rc = host_bytes(tm, tmp_t, &tb);
+    if (rc) return rc;
+    rc = host_bytes(nm, tmp_n, &nb);
+    if (rc) return rc;
+    int depth = 0;
+    rc = check_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, nt, &depth);
+    if (rc) return rc;
+    const rt_cl_triangle* tr = reinterpret_cast<const rt_cl_triangle*>(tb);
+    for (uint32_t i = 0; i < nt; ++i)
+        if (tr[i].mtlIndex >= nmat) return RT_INVALID_MEM_OBJECT;
+
+    if (k->packed_nodes_cap < (size_t)nn) {
+        if (k->packed_nodes) (void)hipFree(k->packed_nodes);
+        k->packed_nodes = nullptr;
+        k->packed_nodes_cap = 0;
+        hipError_t e = hipMalloc(&k->packed_nodes, (size_t)nn * 2 * sizeof(float4));
+        if (e != hipSuccess) return map_hip(e);
+        k->packed_nodes_cap = nn;
+    }
+    if (k->packed_tris_cap < (size_t)nt) {
+        if (k->packed_tris) (void)hipFree(k->packed_tris);
+        k->packed_tris = nullptr;
+        k->packed_tris_cap = 0;
+        hipError_t e = hipMalloc(&k->packed_tris, (size_t)nt * 3 * sizeof(float4));
+        if (e != hipSuccess) return map_hip(e);
+        k->packed_tris_cap = nt;
+    }
+    hipError_t e = rtk::launch_pack(static_cast<const rt_cl_bvh_node*>(nm->dptr), nn, k->packed_nodes,
+                                    static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
+                                    k->ctx->stream);
+    if (e != hipSuccess) return map_hip(e);
+    k->n_nodes = nn;
+    k->n_tris = nt;
+    k->n_mats = nmat;
+    k->depth = depth;
+    k->packed_for_tris = tm;
+    k->packed_tris_gen = tm->generation;
+    k->packed_for_nodes = nm;
+    k->packed_nodes_gen = nm->generation;
+    k->checked_mats = mm;
+    k->checked_mats_gen = mm->generation;
+    return RT_SUCCESS;
+}
+
+hipEvent_t take_event(rt_kernel k) {
+    if (!k->event_pool.empty()) {
+        hipEvent_t e = k->event_pool.back();
+        k->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int drain_events(rt_kernel k) {
+    for (auto& pr : k->pending_events) {
+        float ms = 0.0f;
+        hipError_t e = hipEventSynchronize(pr.second);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
+        if (e != hipSuccess) return map_hip(e);
+        k->kernel_ms += ms;
+        k->event_pool.push_back(pr.first);
+        k->event_pool.push_back(pr.second);
+    }
+    k->pending_events.clear();
+    return RT_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtCreateContext(int device_index, rt_context* out) {
+    if (!out) return RT_INVALID_VALUE;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_DEVICE_NOT_FOUND;
+    if (device_index < 0 || device_index >= n) return RT_INVALID_DEVICE;
+    hipError_t e = hipSetDevice(device_index);
+    if (e != hipSuccess) return map_hip(e);
+    rt_context c = new (std::nothrow) rt_context_s();
+    if (!c) return RT_OUT_OF_HOST_MEMORY;
+    c->device = device_index;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return RT_INVALID_COMMAND_QUEUE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_index) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (c->num_cus <= 0) c->num_cus = 256;
+    *out = c;
+    return RT_SUCCESS;
+}
+
+int rtReleaseContext(rt_context ctx) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RT_SUCCESS;
+}
+
+int rtCreateBuffer(rt_context ctx, uint64_t flags, size_t size, const void* host_ptr, rt_mem* out) {
+    if (!out) return RT_INVALID_VALUE;
+    *out = nullptr;
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (flags & ~kKnownFlags) return RT_INVALID_VALUE;
+    if (size == 0) return RT_INVALID_BUFFER_SIZE;
+    const bool copy = (flags & RT_MEM_COPY_HOST_PTR) != 0;
+    if (copy != (host_ptr != nullptr)) return RT_INVALID_HOST_PTR;
+    rt_mem m = new (std::nothrow) rt_mem_s();
+    if (!m) return RT_OUT_OF_HOST_MEMORY;
+    m->ctx = ctx;
+    m->size = size;
+    m->flags = flags;
+    hipError_t e = hipMalloc(&m->dptr, size);
+    if (e != hipSuccess) {
+        delete m;
+        return map_hip(e);
+    }
+    if (copy) {
+        try {
+            m->shadow.assign(static_cast<const uint8_t*>(host_ptr),
+                             static_cast<const uint8_t*>(host_ptr) + size);
+        } catch (const std::bad_alloc&) {
+            (void)hipFree(m->dptr);
+            delete m;
+            return RT_OUT_OF_HOST_MEMORY;
+        }
+        m->shadow_valid = true;
+        e = hipMemcpyAsync(m->dptr, host_ptr, size, hipMemcpyHostToDevice, ctx->stream);
+    } else {
+        e = hipMemsetAsync(m->dptr, 0, size, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(m->dptr);
+        delete m;
+        return map_hip(e);
+    }
+    *out = m;
+    return RT_SUCCESS;
+}
+
+int rtReleaseBuffer(rt_mem m) {
+    if (!m) return RT_INVALID_MEM_OBJECT;
+    int rc = ensure_device(m->ctx);
+    if (rc) return rc;
+    (void)hipStreamSynchronize(m->ctx->stream);
+    (void)hipFree(m->dptr);
+    delete m;
+    return RT_SUCCESS;
+}
+
+int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
+    if (!out) return RT_INVALID_VALUE;
+    *out = nullptr;
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!name || std::strcmp(name, "KernelEntry") != 0) return RT_INVALID_KERNEL_NAME;
+    rt_kernel k = new (std::nothrow) rt_kernel_s();
+    if (!k) return RT_OUT_OF_HOST_MEMORY;
+    k->ctx = ctx;
+    hipError_t e = hipMalloc(&k->dstats, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, 4 * sizeof(unsigned long long), ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        delete k;
+        return map_hip(e);
+    }
+    *out = k;
+    return RT_SUCCESS;
+}
+
+int rtReleaseKernel(rt_kernel k) {
+    if (!k) return RT_INVALID_KERNEL;
+    int rc = ensure_device(k->ctx);
+    if (rc) return rc;
+    (void)hipStreamSynchronize(k->ctx->stream);
+    for (auto& pr : k->pending_events) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
+    if (k->packed_nodes) (void)hipFree(k->packed_nodes);
+    if (k->packed_tris) (void)hipFree(k->packed_tris);
+    if (k->dstats) (void)hipFree(k->dstats);
+    delete k;
+    return RT_SUCCESS;
+}
+
+int rtSetKernelArg(rt_kernel k, unsigned index, size_t size, const void* value) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (index >= RT_ARG_COUNT) return RT_INVALID_ARG_INDEX;
+    if (!value) return RT_INVALID_ARG_VALUE;
+    if (index <= RT_ARG_BUFFER_MATERIAL) {
+        if (size != sizeof(rt_mem)) return RT_INVALID_ARG_SIZE;
+        rt_mem m = *static_cast<const rt_mem*>(value);
+        if (!m || m->ctx != k->ctx) return RT_INVALID_MEM_OBJECT;
+        k->bufs[index] = m;
+    } else if (index <= RT_ARG_SKYBOX_INTENSITY) {
+        if (size != 4) return RT_INVALID_ARG_SIZE;
+        std::memcpy(&k->u32[index], value, 4);
+    } else {
+        if (size != 16) return RT_INVALID_ARG_SIZE;
+        std::memcpy(k->f3[index - RT_ARG_CAMERA_POS], value, 16);
+    }
+    k->set[index] = true;
+    return RT_SUCCESS;
+}
+
+int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!k || k->ctx != ctx) return RT_INVALID_KERNEL;
+    for (int i = 0; i < RT_ARG_COUNT; ++i)
+        if (!k->set[i]) return RT_INVALID_KERNEL_ARGS;
+    if (global_work_size == 0 || global_work_size > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
+    uint32_t W, H;
+    std::memcpy(&W, &k->u32[RT_ARG_WIDTH], 4);
+    std::memcpy(&H, &k->u32[RT_ARG_HEIGHT], 4);
+    if (W == 0 || H == 0) return RT_INVALID_KERNEL_ARGS;
+    rt_mem out = k->bufs[RT_ARG_BUFFER_OUT];
+    if (out->size < global_work_size * 16) return RT_INVALID_GLOBAL_WORK_SIZE;
+    if (k->hit_ids && (k->hit_ids->size < global_work_size * 4 || k->hit_t->size < global_work_size * 4))
+        return RT_INVALID_MEM_OBJECT;
+    rc = prepare_scene(k);
+    if (rc) return rc;
+
+    uint64_t g0 = std::min<uint64_t>(k->range_first, global_work_size);
+    uint64_t g1 = k->range_last ? std::min<uint64_t>(k->range_last, global_work_size) : global_work_size;
+    if (g1 <= g0) return RT_SUCCESS;  // nothing in range
+
+    rtk::KernelArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.result = static_cast<float4*>(out->dptr);
+    a.trisFull = static_cast<const rt_cl_triangle*>(k->bufs[RT_ARG_BUFFER_SCENE]->dptr);
+    a.materials = static_cast<const rt_cl_material*>(k->bufs[RT_ARG_BUFFER_MATERIAL]->dptr);
+    a.packedNodes = k->packed_nodes;
+    a.packedTris = k->packed_tris;
+    a.nNodes = k->n_nodes;
+    a.nTris = k->n_tris;
+    a.width = W;
+    a.height = H;
+    std::memcpy(&a.frameCount, &k->u32[RT_ARG_FRAME_COUNT], 4);
+    std::memcpy(&a.lightBounces, &k->u32[RT_ARG_LIGHT_BOUNCES], 4);
+    std::memcpy(&a.lightType, &k->u32[RT_ARG_LIGHT_TYPE], 4);
+    std::memcpy(&a.skyboxIntensity, &k->u32[RT_ARG_SKYBOX_INTENSITY], 4);
+    for (int i = 0; i < 3; ++i) {
+        a.camPos[i] = k->f3[0][i];
+        a.camFront[i] = k->f3[1][i];
+        a.camUp[i] = k->f3[2][i];
+    }
+    a.gidBegin = g0;
+    a.gidEnd = g1;
+    const uint64_t row0 = g0 / W, row1 = (g1 + W - 1) / W;
+    a.rowBegin = (uint32_t)row0;
+    a.tilesX = (W + 15) / 16;
+    const uint64_t tilesY = (row1 - row0 + 15) / 16;
+    const uint64_t n_tiles = tilesY * a.tilesX;
+    if (n_tiles > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
+    a.nTiles = (uint32_t)n_tiles;
+    a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
+    a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
+    a.stats = k->dstats;
+
+    const size_t stack_bytes = (size_t)std::max(1, k->depth) * 256 * sizeof(int);
+    const size_t scene_bytes = (size_t)k->n_nodes * 32 + (size_t)k->n_tris * 48;
+    const bool lds = !k->force_global && scene_bytes + stack_bytes <= kLdsBudget;
+    const size_t smem = lds ? scene_bytes + stack_bytes : stack_bytes;
+    if (smem > kLdsBudget) return RT_OUT_OF_RESOURCES;
+    k->last_lds = lds;
+
+    const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;
+    int& occ = k->occ_cache[mi][lds][k->stats];
+    if (occ == 0 || k->occ_smem[mi][lds][k->stats] != smem) {
+        occ = rtk::occupancy_kernel_entry(k->math, lds, k->stats, smem);
+        k->occ_smem[mi][lds][k->stats] = smem;
+    }
+    uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
+    grid = std::min<uint64_t>(grid, n_tiles);
+    if (grid == 0) grid = 1;
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (k->timing) {
+        ev0 = take_event(k);
+        ev1 = take_event(k);
+        if (!ev0 || !ev1) return RT_OUT_OF_RESOURCES;
+        (void)hipEventRecord(ev0, ctx->stream);
+    }
+    hipError_t e = rtk::launch_kernel_entry(a, k->math, lds, k->stats, (unsigned)grid, smem, ctx->stream);
+    if (e != hipSuccess) return map_hip(e);
+    if (k->timing) {
+        (void)hipEventRecord(ev1, ctx->stream);
+        k->pending_events.emplace_back(ev0, ev1);
+        if (k->pending_events.size() > 4096) {
+            rc = drain_events(k);
+            if (rc) return rc;
+        }
+    }
+    ++k->launches;
+    return RT_SUCCESS;
+}
+
+int rtEnqueueReadBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, size_t size, void* dst) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
+    if (!dst || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
+    hipError_t e = hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
+                                  hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && blocking) e = hipStreamSynchronize(ctx->stream);
+    return map_hip(e);
+}
+
+int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, size_t size,
+                         const void* src) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
+    if (!src || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
+    if (m->shadow_valid) std::memcpy(m->shadow.data() + offset, src, size);
+    ++m->generation;
+    hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(m->dptr) + offset, src, size,
+                                  hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && blocking) e = hipStreamSynchronize(ctx->stream);
+    return map_hip(e);
+}
+
+int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem m, size_t offset, size_t size, void* dst) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
+    if (!dst || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
+    return map_hip(hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+}
+
+int rtFinish(rt_context ctx) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    return map_hip(hipStreamSynchronize(ctx->stream));
+}
+
+int rtKernelSetMathMode(rt_kernel k, int mode) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (mode != RT_MATH_PINNED && mode != RT_MATH_DEVICELIB) return RT_INVALID_VALUE;
+    k->math = mode;
+    return RT_SUCCESS;
+}
+
+int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (last != 0 && last < first) return RT_INVALID_VALUE;
+    k->range_first = first;
+    k->range_last = last;
+    return RT_SUCCESS;
+}
+
+int rtKernelSetHitBuffers(rt_kernel k, rt_mem ids, rt_mem t) {
+    if (!k) return RT_INVALID_KERNEL;
+    if ((ids == nullptr) != (t == nullptr)) return RT_INVALID_MEM_OBJECT;
+    if (ids && (ids->ctx != k->ctx || t->ctx != k->ctx)) return RT_INVALID_MEM_OBJECT;
+    k->hit_ids = ids;
+    k->hit_t = t;
+    return RT_SUCCESS;
+}
+
+int rtKernelSetStats(rt_kernel k, int enable) {
+    if (!k) return RT_INVALID_KERNEL;
+    k->stats = enable != 0;
+    return RT_SUCCESS;
+}
+
+int rtKernelSetTiming(rt_kernel k, int enable) {
+    if (!k) return RT_INVALID_KERNEL;
+    k->timing = enable != 0;
+    return RT_SUCCESS;
+}
+
+int rtKernelGetStats(rt_kernel k, rt_stats* out) {
+    if (!k || !out) return RT_INVALID_VALUE;
+    int rc = ensure_device(k->ctx);
+    if (rc) return rc;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(h, k->dstats, sizeof(h), hipMemcpyDeviceToHost, k->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+    if (e != hipSuccess) return map_hip(e);
+    rc = drain_events(k);
+    if (rc) return rc;
+    out->rays = h[0];
+    out->node_visits = h[1];
+    out->tri_tests = h[2];
+    out->hits = h[3];
+    out->launches = k->launches;
+    out->kernel_ms = k->kernel_ms;
+    return RT_SUCCESS;
+}
+
+int rtKernelResetStats(rt_kernel k) {
+    if (!k) return RT_INVALID_KERNEL;
+    int rc = ensure_device(k->ctx);
+    if (rc) return rc;
+    rc = drain_events(k);
+    if (rc) return rc;
+    k->launches = 0;
+    k->kernel_ms = 0.0;
+    hipError_t e = hipMemsetAsync(k->dstats, 0, 4 * sizeof(unsigned long long), k->ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+    return map_hip(e);
+}
+
+int rtKernelGetSceneInLDS(rt_kernel k, int* in_lds) {
+    if (!k || !in_lds) return RT_INVALID_VALUE;
+    *in_lds = k->last_lds ? 1 : 0;
+    return RT_SUCCESS;
+}
+
+int rtKernelForceGlobalScene(rt_kernel k, int force) {
+    if (!k) return RT_INVALID_KERNEL;
+    k->force_global = force != 0;
+    return RT_SUCCESS;
+}
+
+int rtBufferGetDevicePointer(rt_mem m, void** dptr) {
+    if (!m || !dptr) return RT_INVALID_VALUE;
+    *dptr = m->dptr;
+    return RT_SUCCESS;
+}
+
+int rtBufferGetSize(rt_mem m, size_t* size) {
+    if (!m || !size) return RT_INVALID_VALUE;
+    *size = m->size;
+    return RT_SUCCESS;
+}
+
+int rtContextGetStream(rt_context ctx, void** s) {
+    if (!ctx || !s) return RT_INVALID_VALUE;
+    *s = ctx->stream;
+    return RT_SUCCESS;
+}
+
+int rtContextGetDevice(rt_context ctx, int* d) {
+    if (!ctx || !d) return RT_INVALID_VALUE;
+    *d = ctx->device;
+    return RT_SUCCESS;
+}
+
+const char* rtGetBuildInfo(void) {
+    return "librt_hip: KernelEntry for gfx950 (HIP), math modes pinned|devicelib, scene in LDS or HBM";
+}
+
+}  // extern "C"

@@ -1,0 +1,473 @@
+// rt_kernels.hip -- the hot path on gfx950: camera-ray generation, stack-based BVH
+// traversal, Moller-Trumbore triangle test, BRDF bounce loop and gamma accumulation.
+//
+// Replaces KernelEntry (/root/reference/kernel_bvh.cl:415-456) and everything it calls.
+// Written for CDNA4, not translated from the OpenCL source:
+//   * one ray per lane of a wave64; a 256-thread workgroup owns 16x16-pixel tiles
+//     (each wave an 8x8 sub-tile, so neighbouring rays share traversal paths) and walks
+//     them persistently (grid = resident workgroups), so the scene is staged into LDS
+//     once per workgroup, not once per tile;
+//   * BVH nodes are re-packed on the device into 32-byte records (two b128 LDS reads)
+//     and triangles into 48-byte {p1, e1 = p2-p1, e2 = p3-p1} records (three b128
+//     reads); both live in LDS when they fit (Cornell: 4.7 KB), else they are read from
+//     HBM/L2 through the same code (global path);
+//   * the traversal stack is per lane in LDS, laid out [depth][lane] so the 64 lanes of
+//     a wave hit 64 different banks; its depth is the tree depth (host-computed), not
+//     the reference's fixed 64;
+//   * traversal keeps only {t, primitive, u, v}; the hit record (position, shading
+//     normal, material) is formed once after the walk from the last accepted triangle,
+//     which yields the same values as the reference forming it at every accept;
+//   * no MFMA: this is branchy, latency-bound traversal.
+// Parity: every arithmetic step follows the reference's operation order with
+// -ffp-contract=off; transcendentals/dot/normalize come from the math policy
+// (rt_math.hpp).  Hit IDs are indices into the BVH-ordered triangle array, as
+// `isect.object - triangles` in the reference.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_cl_types.h"
+#include "rt_kernels.hpp"
+#include "rt_math.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtk {
+
+constexpr float kTwoPi = 6.28318530718f;    // kernel_bvh.cl:4
+constexpr float kInvPi = 0.31830988618f;    // kernel_bvh.cl:5
+constexpr float kMaxDist = 100000.0f;       // kernel_bvh.cl:7
+constexpr float kHitEps = 1.0e-8f;          // kernel_bvh.cl:101
+
+__device__ __forceinline__ F3 load3(const rt_float3& v) { return F3{v.x, v.y, v.z}; }
+
+// ---- RNG: kernel_bvh.cl:57-71 (integer, bit-exact by construction) ---------------------
+__device__ __forceinline__ uint32_t frame_hash(uint32_t x) { return 1103515245u * x + 12345u; }
+__device__ __forceinline__ float next_rand(uint32_t& s) {
+    uint32_t v = s;
+    v ^= v >> 16;
+    v *= 0x7feb352du;
+    v ^= v >> 15;
+    v *= 0x846ca68bu;
+    v ^= v >> 16;
+    s = v;
+    // float(v) / float(0xffffffff) == float(v) / 2^32, an exact power-of-two scaling
+    return (float)v * 0x1p-32f;
+}
+
+struct Ray {
+    F3 o, d, inv;
+    uint32_t sgn;  // bit i = invDir[i] < 0
+};
+
+// kernel_bvh.cl:42-55
+template <class M>
+__device__ __forceinline__ Ray init_ray(F3 o, F3 d) {
+    Ray r;
+    d = normalize<M>(d);
+    r.o = o;
+    r.d = d;
+    r.inv = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
+    return r;
+}
+
+// kernel_bvh.cl:386-403
+template <class M>
+__device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, F3 pos, F3 front,
+                                          F3 up, float angle, uint32_t& seed) {
+    const float invW = 1.0f / (float)W;
+    const float invH = 1.0f / (float)H;
+    const float aspect = (float)W / (float)H;
+    float x = ((float)(gid % W) + next_rand(seed)) - 0.5f;
+    float y = ((float)(gid / W) + next_rand(seed)) - 0.5f;
+    x = ((2.0f * ((x + 0.5f) * invW) - 1.0f) * angle) * aspect;
+    y = -(1.0f - 2.0f * ((y + 0.5f) * invH)) * angle;
+    F3 dir = ((M::cross(front, up) * x) + (up * y)) + front;
+    return init_ray<M>(pos, normalize<M>(dir));
+}
+
+// ---- scene access ------------------------------------------------------------------------
+// Packed node: q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y, bmax.z, offset, meta),
+// meta = nPrimitives | axis << 16.  Packed triangle: p1, e1, e2 (w unused).
+struct SceneView {
+    const float4* nodes;  // LDS or global
+    const float4* tris;   // LDS or global
+};
+
+struct Traversal {
+    float t;
+    int32_t prim;
+    float u, v;
+};
+
+// kernel_bvh.cl:156-169 (RayBounds).  max/min here only feed comparisons, where the
+// sign of a zero never matters and a NaN operand (0 * inf) must lose -- the fmax/fmin
+// hardware forms give the reference result in both math modes.
+__device__ __forceinline__ bool ray_bounds(const float4 q0, const float4 q1, const Ray& r,
+                                           float t) {
+    const float lox = q0.x, loy = q0.y, loz = q0.z, hix = q0.w, hiy = q1.x, hiz = q1.y;
+    const float nx = (r.sgn & 1u) ? hix : lox, fx = (r.sgn & 1u) ? lox : hix;
+    const float ny = (r.sgn & 2u) ? hiy : loy, fy = (r.sgn & 2u) ? loy : hiy;
+    const float nz = (r.sgn & 4u) ? hiz : loz, fz = (r.sgn & 4u) ? loz : hiz;
+    float t0 = __builtin_fmaxf(0.0f, (nx - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (fx - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (ny - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (fy - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (nz - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (fz - r.o.z) * r.inv.z);
+    return t1 >= t0;
+}
+
+// kernel_bvh.cl:98-153 (RayTriangle), accept test only.
+template <class M>
+__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
+                                             Traversal& h) {
+    const float4 a = tri[0], b = tri[1], c = tri[2];
+    const F3 p1{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
+    const F3 pvec = M::cross(r.d, e2);
+    const float det = M::dot(e1, pvec);
+    if (det < kHitEps) return;  // == (det < 1e-8 || -det > 1e-8); NaN falls through
+    const float inv_det = 1.0f / det;
+    const F3 tvec = r.o - p1;
+    const float u = M::dot(tvec, pvec) * inv_det;
+    if (u < 0.0f || u > 1.0f) return;
+    const F3 qvec = M::cross(tvec, e1);
+    const float v = M::dot(r.d, qvec) * inv_det;
+    if (v < 0.0f || u + v > 1.0f) return;
+    const float t = M::dot(e2, qvec) * inv_det;
+    if (t < h.t) {
+        h.t = t;
+        h.prim = idx;
+        h.u = u;
+        h.v = v;
+    }
+}
+
+// kernel_bvh.cl:171-219 (Intersect).  `stack` points at this lane's column of the
+// workgroup's LDS stack ([depth][256]).
+template <class M, bool kStats>
+__device__ __forceinline__ Traversal intersect(const SceneView& sc, const Ray& r, int* stack,
+                                               uint32_t& visits, uint32_t& tests) {
+    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        const float4 q0 = sc.nodes[2 * cur];
+        const float4 q1 = sc.nodes[2 * cur + 1];
+        if (kStats) ++visits;
+        bool pop = true;
+        if (ray_bounds(q0, q1, r, h.t)) {
+            const uint32_t off = __float_as_uint(q1.z);
+            const uint32_t meta = __float_as_uint(q1.w);
+            const uint32_t np = meta & 0xffffu;
+            if (np > 0) {
+                for (uint32_t i = 0; i < np; ++i) {
+                    if (kStats) ++tests;
+                    ray_triangle<M>(sc.tris + 3 * (size_t)(off + i), (int32_t)(off + i), r, h);
+                }
+            } else {
+                const uint32_t axis = meta >> 16;
+                const bool far_first = (r.sgn >> axis) & 1u;
+                stack[sp * 256] = far_first ? cur + 1 : (int)off;
+                ++sp;
+                cur = far_first ? (int)off : cur + 1;
+                pop = false;
+            }
+        }
+        if (pop) {
+            if (sp == 0) break;
+            --sp;
+            cur = stack[sp * 256];
+        }
+    }
+    return h;
+}
+
+// ---- shading: kernel_bvh.cl:74-90, :221-347 ---------------------------------------------
+template <class M>
+__device__ __forceinline__ void onb(F3 n, F3& s, F3& t) {
+    const F3 axis = pm_fabs(n.x) > 0.001f ? F3{0.0f, 1.0f, 0.0f} : F3{1.0f, 0.0f, 0.0f};
+    t = normalize<M>(M::cross(axis, n));
+    s = M::cross(n, t);
+}
+
+template <class M>
+__device__ __forceinline__ F3 sample_hemisphere_cosine(F3 n, uint32_t& seed) {
+    const float phi = kTwoPi * next_rand(seed);
+    const float s2 = next_rand(seed);
+    const float sinT = __builtin_sqrtf(s2);
+    F3 s, t;
+    onb<M>(n, s, t);
+    const F3 a = (s * M::cos(phi)) * sinT;
+    const F3 b = (t * M::sin(phi)) * sinT;
+    return normalize<M>((a + b) + n * __builtin_sqrtf(1.0f - s2));
+}
+
+template <class M>
+__device__ __forceinline__ F3 sample_ggx(F3 n, float alpha, float& cosTheta, uint32_t& seed) {
+    const float phi = kTwoPi * next_rand(seed);
+    (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
+    const float r = next_rand(seed);
+    cosTheta = M::pow(r, 1.0f / (alpha + 1.0f));
+    const float sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - cosTheta * cosTheta));
+    F3 s, t;
+    onb<M>(n, s, t);
+    const F3 a = (s * M::cos(phi)) * sinT;
+    const F3 b = (t * M::sin(phi)) * sinT;
+    return normalize<M>((a + b) + n * cosTheta);
+}
+
+struct MatView {
+    F3 diffuse, specular, emission;
+    float roughness;
+};
+
+// SampleBrdf (kernel_bvh.cl:294-302) with SampleSpecular (:271-292) and SampleDiffuse
+// (:264-269).  G and F of SampleSpecular are dead in the reference and not evaluated.
+template <class M>
+__device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const MatView& m,
+                                          uint32_t& seed) {
+    if (next_rand(seed) > 0.5f) {
+        float cosTheta = 1.0f;
+        const float alpha = 2.0f / M::pow(m.roughness, 2.0f) - 2.0f;
+        const F3 wh = sample_ggx<M>(n, alpha, cosTheta, seed);
+        wi = (-wo) + wh * (2.0f * M::dot(wo, wh));
+        if (M::dot(wi, n) * M::dot(wo, n) < 0.000001f) return f3s(0.0f);
+        const float a2 = alpha * alpha;
+        const float D = (a2 * kInvPi) / M::pow(cosTheta * cosTheta * (a2 - 1.0f) + 1.0f, 2.0f);
+        pdf = (D * cosTheta) / (4.0f * M::max(M::dot(wo, wh), 0.0f));
+        const float denom =
+            (4.0f * M::max(M::dot(wi, n), 0.0f)) * M::max(M::dot(wo, n), 0.0f) + 0.001f;
+        return m.specular * (D / denom);
+    }
+    wi = sample_hemisphere_cosine<M>(n, seed);
+    pdf = M::dot(wi, n) * kInvPi;
+    return m.diffuse * kInvPi;
+}
+
+// kernel_bvh.cl:304-347
+template <class M>
+__device__ __forceinline__ float light_pixel(const Ray& r, float t, F3 normal, int lightType) {
+    const F3 lightPosition{0.0f, -10.0f, 16.0f};
+    const F3 lightDirection{-0.5f, 0.4f, -0.1f};
+    float intensity = 1.0f, NdotL, attn = 1.0f;
+    if (lightType <= 0) {
+        NdotL = M::max(M::dot(normal, -lightDirection), 0.0f);
+    } else {
+        const F3 X = r.o + r.d * t;
+        const F3 L = lightPosition - X;
+        NdotL = M::max(M::dot(normal, L), 0.0f);
+        if (lightType == 1) {
+            intensity = 16.0f;
+            const float falloff = 0.8f;
+            const F3 eye = L - X;
+            const float d = __builtin_sqrtf(M::dot(eye, eye));
+            attn = (float)(1.0 / (double)(falloff * (d * d)));  // `1.0` is a double literal
+        }
+    }
+    return (attn * intensity) * NdotL;
+}
+
+struct LaneStats {
+    uint32_t rays = 0, visits = 0, tests = 0, hits = 0;
+};
+
+// kernel_bvh.cl:349-384 (Render)
+template <class M, bool kStats>
+__device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* __restrict__ tris_full,
+                                     const rt_cl_material* __restrict__ mats, Ray ray,
+                                     uint32_t& seed, const KernelArgs& a, int* stack,
+                                     int32_t& prim_id, float& prim_t, LaneStats& st) {
+    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
+    const uint32_t bounces = (uint32_t)a.lightBounces;
+    for (uint32_t i = 0; i < bounces; ++i) {
+        if (kStats) ++st.rays;
+        const Traversal h = intersect<M, kStats>(sc, ray, stack, st.visits, st.tests);
+        if (i == 0) {
+            prim_id = h.prim;
+            prim_t = h.t;
+        }
+        if (h.prim < 0) {
+            radiance = radiance + beta * f3s(0.5f * a.skyboxIntensity);
+            break;
+        }
+        if (kStats) ++st.hits;
+        // hit record of the last accepted triangle (kernel_bvh.cl:142-147)
+        const rt_cl_triangle& tri = tris_full[h.prim];
+        const float w = (1.0f - h.u) - h.v;
+        const F3 normal = normalize<M>((load3(tri.v2.normal) * h.u + load3(tri.v3.normal) * h.v) +
+                                       load3(tri.v1.normal) * w);
+        const F3 pos = ray.o + ray.d * h.t;
+        const rt_cl_material& mm = mats[tri.mtlIndex];
+        MatView m{load3(mm.diffuse), load3(mm.specular), load3(mm.emission), mm.roughness};
+
+        radiance = radiance + (beta * m.emission) * 50.0f;
+        F3 wi = f3s(0.0f);
+        float pdf = 0.0f;
+        const F3 f = sample_brdf<M>(-ray.d, wi, pdf, normal, m, seed);
+        if (pdf <= 0.0f || pdf != pdf) break;
+        const F3 mul = (f * M::dot(wi, normal)) / pdf;
+        beta = beta * mul;
+        const float lp = light_pixel<M>(ray, h.t, normal, a.lightType);
+        radiance = radiance + (f3s(lp) * m.diffuse) * beta;
+        ray = init_ray<M>(pos + wi * 0.01f, wi);
+    }
+    return F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
+    unsigned long long x = v;
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+// ---- the kernel ---------------------------------------------------------------------------
+template <class M, bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int tid = threadIdx.x;
+    const float4* nodes;
+    const float4* tris;
+    int* stack_base;
+    if (kLdsScene) {
+        float4* ln = smem;
+        float4* lt = smem + 2 * a.nNodes;
+        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
+        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+        nodes = ln;
+        tris = lt;
+        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
+        __syncthreads();
+    } else {
+        nodes = a.packedNodes;
+        tris = a.packedTris;
+        stack_base = reinterpret_cast<int*>(smem);
+    }
+    int* stack = stack_base + tid;
+    const SceneView sc{nodes, tris};
+
+    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
+    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
+    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
+    // tan(0.5f * (45.0f * 3.1415f / 180.0f)), kernel_bvh.cl:392
+    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));
+    const uint32_t fh = frame_hash(a.frameCount);
+
+    const int wave = tid >> 6, lane = tid & 63;
+    const uint32_t dx = (uint32_t)((wave & 1) * 8 + (lane & 7));
+    const uint32_t dy = (uint32_t)((wave >> 1) * 8 + (lane >> 3));
+
+    LaneStats st;
+    for (uint32_t tile = blockIdx.x; tile < a.nTiles; tile += gridDim.x) {
+        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+        const uint32_t x = tx * 16 + dx;
+        const uint32_t row = a.rowBegin + ty * 16 + dy;
+        const uint64_t g64 = (uint64_t)row * a.width + x;
+        if (x >= a.width || g64 < a.gidBegin || g64 >= a.gidEnd) continue;
+        const uint32_t gid = (uint32_t)g64;
+
+        uint32_t seed = gid + fh;  // kernel_bvh.cl:445
+        const Ray ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+        int32_t pid = -1;
+        float pt = 0.0f;
+        const F3 rad = render<M, kStats>(sc, a.trisFull, a.materials, ray, seed, a, stack, pid, pt, st);
+
+        // kernel_bvh.cl:449-455
+        F3 out;
+        if (a.frameCount == 0) {
+            out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
+        } else {
+            const float4 old = a.result[gid];
+            const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
+            const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
+            const F3 acc = ((lin * fm1) + rad) / fc;
+            out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+        }
+        a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
+        if (a.hitIds) {
+            a.hitIds[gid] = pid;
+            a.hitT[gid] = pt;
+        }
+    }
+    if (kStats) {
+        const unsigned long long r = wave_sum(st.rays), v = wave_sum(st.visits), t = wave_sum(st.tests),
+                       h = wave_sum(st.hits);
+        if (lane == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[0]), (unsigned long long)r);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[1]), (unsigned long long)v);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[2]), (unsigned long long)t);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[3]), (unsigned long long)h);
+        }
+    }
+}
+
+// ---- scene packing (runs once per bound scene) -----------------------------------------------
+__global__ void pack_nodes(const rt_cl_bvh_node* __restrict__ in, float4* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rt_cl_bvh_node nd = in[i];
+    const uint32_t meta = (uint32_t)nd.nPrimitives | ((uint32_t)(nd.nPrimitives ? 0 : nd.axis) << 16);
+    out[2 * i] = make_float4(nd.bounds.pmin.x, nd.bounds.pmin.y, nd.bounds.pmin.z, nd.bounds.pmax.x);
+    out[2 * i + 1] = make_float4(nd.bounds.pmax.y, nd.bounds.pmax.z, __uint_as_float(nd.offset),
+                                 __uint_as_float(meta));
+}
+
+__global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rt_float3 p1 = in[i].v1.position, p2 = in[i].v2.position, p3 = in[i].v3.position;
+    // e1 = t2 - t1, e2 = t3 - t1 exactly as kernel_bvh.cl:109-110 computes them
+    out[3 * i] = make_float4(p1.x, p1.y, p1.z, 0.0f);
+    out[3 * i + 1] = make_float4(p2.x - p1.x, p2.y - p1.y, p2.z - p1.z, 0.0f);
+    out[3 * i + 2] = make_float4(p3.x - p1.x, p3.y - p1.y, p3.z - p1.z, 0.0f);
+}
+
+}  // namespace rtk
+
+// ---- host-side launch helpers ------------------------------------------------------------
+namespace rtk {
+
+template <class M, bool L, bool S>
+static hipError_t launch_one(const KernelArgs& a, unsigned grid, size_t smem, hipStream_t st) {
+    hipLaunchKernelGGL((kernel_entry<M, L, S>), dim3(grid), dim3(256), smem, st, a);
+    return hipGetLastError();
+}
+
+template <class M, bool L, bool S>
+static int occupancy_one(size_t smem) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel_entry<M, L, S>, 256, smem) !=
+        hipSuccess)
+        return 1;
+    return blocks > 0 ? blocks : 1;
+}
+
+hipError_t launch_kernel_entry(const KernelArgs& a, int math, bool lds, bool stats, unsigned grid,
+                               size_t smem, hipStream_t st) {
+#define RTK_DISPATCH(MM)                                                           \
+    if (lds) return stats ? launch_one<MM, true, true>(a, grid, smem, st)          \
+                          : launch_one<MM, true, false>(a, grid, smem, st);        \
+    return stats ? launch_one<MM, false, true>(a, grid, smem, st)                  \
+                 : launch_one<MM, false, false>(a, grid, smem, st);
+    if (math == MathDeviceLib::kId) { RTK_DISPATCH(MathDeviceLib) }
+    RTK_DISPATCH(MathPinned)
+#undef RTK_DISPATCH
+}
+
+int occupancy_kernel_entry(int math, bool lds, bool stats, size_t smem) {
+#define RTK_OCC(MM)                                                                        \
+    if (lds) return stats ? occupancy_one<MM, true, true>(smem) : occupancy_one<MM, true, false>(smem); \
+    return stats ? occupancy_one<MM, false, true>(smem) : occupancy_one<MM, false, false>(smem);
+    if (math == MathDeviceLib::kId) { RTK_OCC(MathDeviceLib) }
+    RTK_OCC(MathPinned)
+#undef RTK_OCC
+}
+
+hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
+                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, hipStream_t st) {
+    if (n_nodes) hipLaunchKernelGGL(pack_nodes, dim3((n_nodes + 255) / 256), dim3(256), 0, st, nodes, pn, n_nodes);
+    if (n_tris) hipLaunchKernelGGL(pack_tris, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, pt, n_tris);
+    return hipGetLastError();
+}
+
+}  // namespace rtk

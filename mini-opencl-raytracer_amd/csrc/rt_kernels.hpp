@@ -1,0 +1,40 @@
+// rt_kernels.hpp -- launch interface between the C ABI (rt_capi.cpp) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_cl_types.h"
+
+namespace rtk {
+
+// Everything KernelEntry's 14 arguments carry (kernel_bvh.cl:415-431), plus the packed
+// scene, the work-item range of this launch and the optional extension outputs.
+struct KernelArgs {
+    float4* result;                     // slot 0: float3 per work-item, 16-byte stride
+    const rt_cl_triangle* trisFull;     // slot 1 (normals, material index)
+    const rt_cl_material* materials;    // slot 3
+    const float4* packedNodes;          // derived from slot 2: 2 x float4 per node
+    const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
+    uint32_t nNodes, nTris;
+    uint32_t width, height;             // slots 4, 5
+    uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)
+    int32_t lightBounces, lightType;    // slots 8, 9
+    float skyboxIntensity;              // slot 10
+    float camPos[3], camFront[3], camUp[3];  // slots 11-13 (w ignored)
+    // work decomposition: work-items [gidBegin, gidEnd), rows [rowBegin, rowEnd)
+    uint64_t gidBegin, gidEnd;
+    uint32_t rowBegin, tilesX, nTiles;
+    // extensions
+    int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
+    float* hitT;                        // primary isect.t per work-item
+    unsigned long long* stats;          // [rays, node visits, triangle tests, hits]
+};
+
+hipError_t launch_kernel_entry(const KernelArgs& a, int math, bool lds, bool stats, unsigned grid,
+                               size_t smem, hipStream_t st);
+int occupancy_kernel_entry(int math, bool lds, bool stats, size_t smem);
+hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
+                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, hipStream_t st);
+
+}  // namespace rtk

@@ -1,0 +1,99 @@
+// rt_math.hpp -- float3 algebra and the two math policies of the HIP hot path.
+//
+// MathPinned   : the pinned builtin semantics of include/rt_pinned_math.h (identical,
+//                bit for bit, to the CPU oracle; no hardware approximations).
+// MathDeviceLib: the semantics the AMD OpenCL toolchain gives the reference kernel on
+//                this GPU (device library opencl.bc / ocml.bc): dot/cross with fma
+//                (opencl.bc _Z3dotDv3_fS_, _Z5crossDv3_fS_), normalize = v * rsqrt(d)
+//                with the hardware-rsq based __ocml_rsqrt_f32 (_Z9normalizeDv3_f),
+//                pow/sin/cos/tan = __ocml_*_f32, max/min = llvm.maxnum/minnum.  This is
+//                the mode that is checked against the reference kernel itself, built by
+//                the image's OpenCL compiler and run through the OpenCL runtime
+//                (oracle/_ref, tests/test_ref_opencl.py).
+//
+// Everything here is compiled with -ffp-contract=off: each + - * / below is one IEEE
+// operation, in the association order the reference source spells out.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_pinned_math.h"
+
+#pragma clang fp contract(off)
+
+namespace rtk {
+
+struct F3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 f3s(float s) { return F3{s, s, s}; }
+__device__ __forceinline__ F3 operator+(F3 a, F3 b) { return F3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ F3 operator-(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ F3 operator*(F3 a, F3 b) { return F3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ F3 operator*(F3 a, float s) { return F3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ F3 operator/(F3 a, float s) { return F3{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
+
+// ---------------------------------------------------------------------------------------
+struct MathPinned {
+    static constexpr int kId = 0;
+    __device__ __forceinline__ static float dot(F3 a, F3 b) {
+        return (a.x * b.x + a.y * b.y) + a.z * b.z;
+    }
+    __device__ __forceinline__ static F3 cross(F3 a, F3 b) {
+        return F3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+    }
+    __device__ __forceinline__ static float rsqrt(float d) { return pm_rsqrt(d); }
+    __device__ __forceinline__ static float pow(float x, float y) { return pm_pow(x, y); }
+    __device__ __forceinline__ static float sin(float x) { return pm_sin(x); }
+    __device__ __forceinline__ static float cos(float x) { return pm_cos(x); }
+    __device__ __forceinline__ static float tan(float x) { return pm_tan(x); }
+    __device__ __forceinline__ static float max(float x, float y) { return pm_max(x, y); }
+    __device__ __forceinline__ static float min(float x, float y) { return pm_min(x, y); }
+};
+
+struct MathDeviceLib {
+    static constexpr int kId = 1;
+    // opencl.bc: dot = fma(z, z', fma(y, y', x*x'))
+    __device__ __forceinline__ static float dot(F3 a, F3 b) {
+        return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+    }
+    // opencl.bc: cross.x = fma(a.y, b.z, b.y * -a.z), ...
+    __device__ __forceinline__ static F3 cross(F3 a, F3 b) {
+        return F3{__builtin_fmaf(a.y, b.z, b.y * -a.z), __builtin_fmaf(a.z, b.x, b.z * -a.x),
+                  __builtin_fmaf(a.x, b.y, b.x * -a.y)};
+    }
+    __device__ __forceinline__ static float rsqrt(float d) { return ::rsqrtf(d); }
+    __device__ __forceinline__ static float pow(float x, float y) { return ::powf(x, y); }
+    __device__ __forceinline__ static float sin(float x) { return ::sinf(x); }
+    __device__ __forceinline__ static float cos(float x) { return ::cosf(x); }
+    __device__ __forceinline__ static float tan(float x) { return ::tanf(x); }
+    __device__ __forceinline__ static float max(float x, float y) { return __builtin_fmaxf(x, y); }
+    __device__ __forceinline__ static float min(float x, float y) { return __builtin_fminf(x, y); }
+};
+
+// normalize with the guard structure shared by both policies (see rt_pinned_math.h)
+template <class M>
+__device__ __forceinline__ F3 normalize(F3 v) {
+    if (v.x == 0.0f && v.y == 0.0f && v.z == 0.0f) return v;
+    float d = M::dot(v, v);
+    if (d < 0x1p-126f) {
+        v = v * 0x1p86f;
+        d = M::dot(v, v);
+    } else if (pm_isinf(d)) {
+        v = v * 0x1p-66f;
+        d = M::dot(v, v);
+        if (pm_isinf(d)) {
+            v = F3{pm_copysign(pm_isinf(v.x) ? 1.0f : 0.0f, v.x),
+                   pm_copysign(pm_isinf(v.y) ? 1.0f : 0.0f, v.y),
+                   pm_copysign(pm_isinf(v.z) ? 1.0f : 0.0f, v.z)};
+            d = M::dot(v, v);
+        }
+    }
+    return v * M::rsqrt(d);
+}
+
+}  // namespace rtk

@@ -1,0 +1,131 @@
+// rt_render.cpp -- command-line host: the reference's render loop without the window.
+//
+// Follows CLEngineBase::renderLoop (CLEngineBase.cpp:166-222) and CLRaytracer
+// (CLRaytracer.cpp:12-148) through the reference-shaped C++ wrapper: Init (context +
+// kernel + output buffer), CLOBJloader::Load + CreateBVHTrees + SetupBuffers, then
+// RenderFrame per frame (uniforms, ExecuteKernel(W*H), ReadBuffer, Finish,
+// ++m_FrameCount).  The GL blit is replaced by a PPM writer (rows flipped: row 0 of the
+// output is the bottom of the image, as glTexSubImage2D shows it).
+//
+// usage: rt_render [obj=path] [w=W] [h=H] [frames=N] [bounces=B] [light=T] [sky=S]
+//                  [out=file.ppm] [device=D] [math=pinned|devicelib]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_cl_compat.hpp"
+#include "../../include/rt_scene.h"
+
+using rtcl::RenderKernelArgument_t;
+
+namespace {
+
+struct HostFloat3 {  // the reference host float3 (CLmathlib.hpp:18-54): 16 bytes
+    float x, y, z, w;
+};
+
+std::string arg(int argc, char** argv, const char* key, const char* dflt) {
+    const size_t n = std::strlen(key);
+    for (int i = 1; i < argc; ++i)
+        if (std::strncmp(argv[i], key, n) == 0 && argv[i][n] == '=') return argv[i] + n + 1;
+    return dflt;
+}
+
+void write_ppm(const char* path, const std::vector<float>& px, unsigned W, unsigned H) {
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return;
+    std::fprintf(f, "P6\n%u %u\n255\n", W, H);
+    std::vector<unsigned char> row(3 * (size_t)W);
+    for (unsigned y = 0; y < H; ++y) {
+        const unsigned src = H - 1 - y;
+        for (unsigned x = 0; x < W; ++x)
+            for (int c = 0; c < 3; ++c) {
+                float v = px[4 * ((size_t)src * W + x) + c];
+                v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+                row[3 * x + c] = (unsigned char)(v * 255.0f + 0.5f);
+            }
+        std::fwrite(row.data(), 1, row.size(), f);
+    }
+    std::fclose(f);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const std::string obj = arg(argc, argv, "obj", "scenes/cornell.obj");
+    const unsigned W = (unsigned)std::atoi(arg(argc, argv, "w", "1920").c_str());
+    const unsigned H = (unsigned)std::atoi(arg(argc, argv, "h", "1080").c_str());
+    const int frames = std::atoi(arg(argc, argv, "frames", "8").c_str());
+    int lightBounces = std::atoi(arg(argc, argv, "bounces", "9").c_str());  // CLRaytracer.h:32
+    int lightType = std::atoi(arg(argc, argv, "light", "0").c_str());       // CLRaytracer.h:31
+    float skybox = (float)std::atof(arg(argc, argv, "sky", "1.0").c_str()); // CLRaytracer.h:34
+    const std::string out = arg(argc, argv, "out", "render.ppm");
+    const int device = std::atoi(arg(argc, argv, "device", "0").c_str());
+    const bool devlib = arg(argc, argv, "math", "pinned") == "devicelib";
+
+    try {
+        // CLRaytracer::Init (CLRaytracer.cpp:104-120)
+        rtcl::CLContext ctx(device);
+        auto kernel = std::make_shared<rtcl::CLKernel>(ctx, "KernelEntry");
+        if (devlib) rtcl::check(rtKernelSetMathMode(kernel->GetKernel(), RT_MATH_DEVICELIB), "math mode");
+        // CLRaytracer::SetupBuffers (CLRaytracer.cpp:122-137)
+        int wi = (int)W, hi = (int)H;
+        kernel->SetArgument(RenderKernelArgument_t::WIDTH, &wi, sizeof(int));
+        kernel->SetArgument(RenderKernelArgument_t::HEIGHT, &hi, sizeof(int));
+        std::vector<float> pixels(4 * (size_t)W * H);
+        rtcl::Buffer output(ctx.GetContext(), RT_MEM_WRITE_ONLY, (size_t)W * H * 16);
+        kernel->SetBuffer(RenderKernelArgument_t::BUFFER_OUT, output);
+
+        // CLOBJloader::Load + CLBVHScene::CreateBVHTrees (CLEngineBase.cpp:173-179)
+        rt_scene* scene = nullptr;
+        rtcl::check(rtsLoadOBJ(obj.c_str(), 4, &scene), "Failed to load scene");
+        const rt_cl_triangle* tris;
+        const rt_cl_bvh_node* nodes;
+        const rt_cl_material* mats;
+        size_t nt, nn, nm;
+        rtsGetTriangles(scene, &tris, &nt);
+        rtsGetNodes(scene, &nodes, &nn);
+        rtsGetMaterials(scene, &mats, &nm);
+        // CLBVHScene::SetupBuffers (CLBVHnode.cpp:209-236)
+        const uint64_t ro = RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
+        rtcl::Buffer tb(ctx.GetContext(), ro, nt * sizeof(rt_cl_triangle), tris);
+        rtcl::Buffer nb(ctx.GetContext(), ro, nn * sizeof(rt_cl_bvh_node), nodes);
+        rtcl::Buffer mb(ctx.GetContext(), ro, nm * sizeof(rt_cl_material), mats);
+        kernel->SetBuffer(RenderKernelArgument_t::BUFFER_SCENE, tb);
+        kernel->SetBuffer(RenderKernelArgument_t::BUFFER_NODE, nb);
+        kernel->SetBuffer(RenderKernelArgument_t::BUFFER_MATERIAL, mb);
+        rtsRelease(scene);
+
+        // CLCamera defaults (CLcamera.h:8-10)
+        HostFloat3 pos{0.0f, -25.0f, 8.5f, 0.0f}, front{0.0f, 1.0f, 0.0f, 0.0f}, up{0.0f, 0.0f, 1.0f, 0.0f};
+        unsigned frameCount = 1;  // m_FrameCount (CLRaytracer.h:30)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int f = 0; f < frames; ++f) {
+            // CLRaytracer::RenderFrame (CLRaytracer.cpp:35-56, 101)
+            unsigned seed = (unsigned)std::rand();
+            kernel->SetArgument(RenderKernelArgument_t::FRAME_COUNT, &frameCount, sizeof(unsigned));
+            kernel->SetArgument(RenderKernelArgument_t::FRAME_SEED, &seed, sizeof(unsigned));
+            kernel->SetArgument(RenderKernelArgument_t::LIGHT_BOUNCES, &lightBounces, sizeof(int));
+            kernel->SetArgument(RenderKernelArgument_t::LIGHT_TYPE, &lightType, sizeof(int));
+            kernel->SetArgument(RenderKernelArgument_t::SKYBOX_INTENSITY, &skybox, sizeof(float));
+            kernel->SetArgument(RenderKernelArgument_t::CAMERA_POS, &pos, sizeof(HostFloat3));
+            kernel->SetArgument(RenderKernelArgument_t::CAMERA_FRONT, &front, sizeof(HostFloat3));
+            kernel->SetArgument(RenderKernelArgument_t::CAMERA_UP, &up, sizeof(HostFloat3));
+            ctx.ExecuteKernel(kernel, (size_t)W * H);
+            ctx.ReadBuffer(output, pixels.data(), 16 * (size_t)W * H);
+            ctx.Finish();
+            ++frameCount;
+        }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("rendered %d frame(s) %ux%u, %d bounces: %.3f ms/frame (incl. readback)\n", frames, W, H,
+                    lightBounces, ms / (frames > 0 ? frames : 1));
+        write_ppm(out.c_str(), pixels, W, H);
+    } catch (const rtcl::CLException& ex) {
+        std::fprintf(stderr, "Caught exception: %s\n", ex.what());
+        return 1;
+    }
+    return 0;
+}

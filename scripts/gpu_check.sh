@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, short bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; the script stops at the first step that
+# crashed, aborted or timed out (exit >= 124 or a signal), and continues past plain
+# test failures (exit 1) so one call still yields a bench line and a profile.
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # run <name> <timeout-s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/steps.log
+  tail -5 $OUT/$name.log
+  if [ $rc -ge 124 ] || [ $rc -gt 1 ] && [ $rc -ne 5 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a $OUT/steps.log
+    exit $rc
+  fi
+  return 0
+}
+(clinfo 2>&1 | head -60 > $OUT/clinfo.txt) || true
+(rocm-smi --showproductname 2>&1 | head -20 > $OUT/smi.txt) || true
+nproc > $OUT/nproc.txt; (lscpu | head -20 >> $OUT/nproc.txt) || true
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    benchdl) run bench_devicelib 600 python bench.py --math devicelib --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
