@@ -19,6 +19,10 @@
  *   - max/min    = OpenCL fmax/fmin for NaN (the non-NaN operand wins) and the OpenCL
  *                  common-function tie rule otherwise (max: y if x < y else x;
  *                  min: y if y < x else x) -- this fixes the sign of zero results;
+ *   - pow(x, 2.0f) written with a literal 2 (kernel_bvh.cl:224, :275) = x*x, the
+ *                  correctly rounded square (LLVM's generic and AMDGPU libcall
+ *                  simplifiers both fold it so; the AMD OpenCL build of the reference
+ *                  does, see its IR);
  *   - sin/cos/tan/pow = fp64 evaluation (Cody-Waite reduction, fdlibm-style kernels,
  *                  atanh-series log, Taylor exp2) rounded once to fp32.  Results are
  *                  faithful (correctly rounded except in rare near-midpoint cases) and,
@@ -79,6 +83,9 @@ RT_PM_FN float pm_min(float x, float y) {
 }
 
 RT_PM_FN float pm_rsqrt(float d) { return 1.0f / pm_sqrt(d); }
+
+/* pow(x, 2.0f) with a literal exponent */
+RT_PM_FN float pm_sq(float x) { return x * x; }
 
 /* ---- fp64 helpers ------------------------------------------------------------------ */
 /* round-to-nearest-even integer value of |x| < 2^51 via the 1.5*2^52 shifter */

@@ -229,12 +229,12 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
                                           uint32_t& seed) {
     if (next_rand(seed) > 0.5f) {
         float cosTheta = 1.0f;
-        const float alpha = 2.0f / M::pow(m.roughness, 2.0f) - 2.0f;
+        const float alpha = 2.0f / M::pow2(m.roughness) - 2.0f;
         const F3 wh = sample_ggx<M>(n, alpha, cosTheta, seed);
         wi = (-wo) + wh * (2.0f * M::dot(wo, wh));
         if (M::dot(wi, n) * M::dot(wo, n) < 0.000001f) return f3s(0.0f);
         const float a2 = alpha * alpha;
-        const float D = (a2 * kInvPi) / M::pow(cosTheta * cosTheta * (a2 - 1.0f) + 1.0f, 2.0f);
+        const float D = (a2 * kInvPi) / M::pow2(cosTheta * cosTheta * (a2 - 1.0f) + 1.0f);
         pdf = (D * cosTheta) / (4.0f * M::max(M::dot(wo, wh), 0.0f));
         const float denom =
             (4.0f * M::max(M::dot(wi, n), 0.0f)) * M::max(M::dot(wo, n), 0.0f) + 0.001f;

@@ -48,6 +48,9 @@ struct MathPinned {
     }
     __device__ __forceinline__ static float rsqrt(float d) { return pm_rsqrt(d); }
     __device__ __forceinline__ static float pow(float x, float y) { return pm_pow(x, y); }
+    // pow(x, 2.0f) call sites of the reference (kernel_bvh.cl:224, :275): pinned as the
+    // exact square, as LLVM's libcall simplifiers fold it (rt_pinned_math.h)
+    __device__ __forceinline__ static float pow2(float x) { return pm_sq(x); }
     __device__ __forceinline__ static float sin(float x) { return pm_sin(x); }
     __device__ __forceinline__ static float cos(float x) { return pm_cos(x); }
     __device__ __forceinline__ static float tan(float x) { return pm_tan(x); }
@@ -68,6 +71,9 @@ struct MathDeviceLib {
     }
     __device__ __forceinline__ static float rsqrt(float d) { return ::rsqrtf(d); }
     __device__ __forceinline__ static float pow(float x, float y) { return ::powf(x, y); }
+    // the AMD OpenCL compiler folds pow(x, 2.0f) to x*x (AMDGPU libcall simplification;
+    // visible in the reference's IR: DistributionGGX, SampleSpecular)
+    __device__ __forceinline__ static float pow2(float x) { return x * x; }
     __device__ __forceinline__ static float sin(float x) { return ::sinf(x); }
     __device__ __forceinline__ static float cos(float x) { return ::cosf(x); }
     __device__ __forceinline__ static float tan(float x) { return ::tanf(x); }

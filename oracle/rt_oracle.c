@@ -241,7 +241,7 @@ static o_isect o_intersect(const o_ray* ray, const o_scene* sc, o_counts* cnt) {
 /* kernel_bvh.cl:221-225 */
 static float o_distribution_ggx(float c, float alpha) {
     float a2 = alpha * alpha;
-    return a2 * O_INV_PI / pm_pow(c * c * (a2 - 1.0f) + 1.0f, 2.0f);
+    return a2 * O_INV_PI / pm_sq(c * c * (a2 - 1.0f) + 1.0f); /* pow(., 2.0f) */
 }
 
 /* kernel_bvh.cl:227-239 */
@@ -270,7 +270,7 @@ static of3 o_sample_diffuse(of3* wi, float* pdf, of3 n, const o_mat* m, uint32_t
  * (`G` and `F` are never read) and have no side effects, so they are not evaluated. */
 static of3 o_sample_specular(of3 wo, of3* wi, float* pdf, of3 n, const o_mat* m, uint32_t* seed) {
     float cosTheta = 1.0f;
-    float alpha = 2.0f / pm_pow(m->roughness, 2.0f) - 2.0f;
+    float alpha = 2.0f / pm_sq(m->roughness) - 2.0f; /* pow(roughness, 2.0f) */
     of3 wh = o_sample_ggx(n, alpha, &cosTheta, seed);
     *wi = o_reflect(wo, wh);
     if (vdot(*wi, n) * vdot(wo, n) < 0.000001f) return vs(0.0f);

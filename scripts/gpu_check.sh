@@ -30,6 +30,9 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     benchdl) run bench_devicelib 600 python bench.py --math devicelib --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline && \
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Run the REFERENCE kernel (oracle/_ref: /root/reference/kernel_bvh.cl compiled by the
+image's OpenCL compiler) on the GPU box through the OpenCL runtime and store its outputs
+as golden fixtures (tests/golden/ref_*.npz).  Also prints how the HIP path (both math
+modes) and the CPU oracle compare with it.
+
+  python scripts/make_ref_goldens.py [outdir]      (default gpurun_out/golden)
+
+Fixtures (all Cornell, default camera, lightType 0, sky 1.0):
+  ref_{variant}_hits_{W}x{H}.npz      frame-1 primary hit ids + t (PrimaryHitEntry harness)
+  ref_{variant}_rad_{W}x{H}_b{B}_f{F}.npz  KernelEntry output after frames 1..F (float32 RGB)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "mini-opencl-raytracer_amd"), os.path.join(REPO, "oracle"),
+          os.path.join(REPO, "tests")):
+    sys.path.insert(0, p)
+
+import clref  # noqa: E402
+import clrt  # noqa: E402
+import oracle  # noqa: E402
+from clrt import _native as N  # noqa: E402
+from hip_helpers import HipRenderer  # noqa: E402
+
+HIT_CONFIGS = [(128, 72), (512, 512), (1920, 1080)]
+RAD_CONFIGS = [(128, 72, 1, 1), (128, 72, 2, 1), (128, 72, 9, 1), (128, 72, 9, 8), (512, 512, 9, 8),
+               (1920, 1080, 2, 1)]
+
+
+def cmp_bits(a, b):
+    a = np.ascontiguousarray(a).view(np.uint32).ravel()
+    b = np.ascontiguousarray(b).view(np.uint32).ravel()
+    return int((a != b).sum())
+
+
+def rel_err(a, b):
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    m = np.maximum(np.abs(a), np.abs(b)).astype(np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.where(m > 0, d / m, 0.0)
+    return float(np.nanmax(r)) if r.size else 0.0
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "golden")
+    os.makedirs(out, exist_ok=True)
+    scene = clrt.scene.cornell()
+    ok, why = clref.available()
+    if not ok:
+        print("reference runner unavailable:", why)
+        return 2
+    for variant in ("strict", "shipped"):
+        ref = clref.ReferenceKernel(variant)
+        print(f"== reference variant {variant} on OpenCL device '{ref.device_name}'")
+        for (W, H) in HIT_CONFIGS:
+            t0 = time.time()
+            ids, t = ref.primary_hits(scene, W, H)
+            np.savez_compressed(os.path.join(out, f"ref_{variant}_hits_{W}x{H}.npz"), ids=ids, t=t)
+            _, oids, ot, _ = oracle.render(scene, W, H, frame_count=1, light_bounces=1, want_hits=True, threads=16)
+            line = f"hits {W}x{H}: ref hits={int((ids >= 0).sum())} ({time.time() - t0:.2f}s) | oracle(pinned) ids differ {int((ids != oids).sum())} t bits {cmp_bits(t, ot)}"
+            for mode, name in ((N.MATH_DEVICELIB, "hip-devicelib"), (N.MATH_PINNED, "hip-pinned")):
+                r = HipRenderer(scene, W, H, math=mode, hits=True)
+                r.frame(1, light_bounces=1)
+                hids, ht = r.hits()
+                r.close()
+                line += f" | {name} ids differ {int((ids != hids).sum())} t bits {cmp_bits(t, ht)}"
+            print(line, flush=True)
+        for (W, H, B, F) in RAD_CONFIGS:
+            frames = range(1, F + 1)
+            rad = ref.render(scene, W, H, frames=frames, light_bounces=B)[:, :3].copy()
+            np.savez_compressed(os.path.join(out, f"ref_{variant}_rad_{W}x{H}_b{B}_f{F}.npz"), rgb=rad)
+            res = np.zeros((W * H, 4), np.float32)
+            for f in frames:
+                res, _, _, _ = oracle.render(scene, W, H, frame_count=f, light_bounces=B, result=res, threads=16)
+            line = (f"rad {W}x{H} b{B} f{F}: oracle words differ {cmp_bits(rad, res[:, :3])} "
+                    f"maxrel {rel_err(rad, res[:, :3]):.3g}")
+            for mode, name in ((N.MATH_DEVICELIB, "hip-devicelib"), (N.MATH_PINNED, "hip-pinned")):
+                r = HipRenderer(scene, W, H, math=mode)
+                for f in frames:
+                    r.frame(f, light_bounces=B)
+                got = r.result()[:, :3]
+                r.close()
+                line += f" | {name} words differ {cmp_bits(rad, got)} maxrel {rel_err(rad, got):.3g}"
+            print(line, flush=True)
+        ref.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
