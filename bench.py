@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--bounces", type=int, default=9)
     p.add_argument("--math", choices=["pinned", "devicelib"], default="pinned")
+    p.add_argument("--sched", choices=["regen", "tiles"], default="regen")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     return p.parse_args()
@@ -87,6 +88,7 @@ class Rank:
         k.set_float3(N.CAMERA_FRONT, CAMERA[1])
         k.set_float3(N.CAMERA_UP, CAMERA[2])
         k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
+        k.set_schedule(N.SCHED_TILES if args.sched == "tiles" else N.SCHED_REGEN)
         k.set_work_range(self.row0 * W, self.row1 * W)
 
     def render(self):
@@ -243,7 +245,7 @@ def main():
         "data": "reference scene cornell.obj (scenes/cornell_scene.npz); rays generated in-kernel",
         "config": {"workload": f"cornell {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "parallelism": f"row tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
+                   "math": args.math, "schedule": args.sched, "parallelism": f"row tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

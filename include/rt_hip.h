@@ -107,6 +107,14 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset
 #define RT_MATH_DEVICELIB 1
 int rtKernelSetMathMode(rt_kernel k, int mode);
 
+/* Work schedule of the kernel (same results, different lane scheduling):
+ * RT_SCHED_REGEN (default) -- persistent lanes; a lane whose path ends starts the next
+ *                             pixel of its wave's 8x8 chunk (path regeneration);
+ * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles). */
+#define RT_SCHED_TILES 0
+#define RT_SCHED_REGEN 1
+int rtKernelSetSchedule(rt_kernel k, int sched);
+
 /* Restrict the next launches to work-items [first, last) (pixel-row tiles for
  * multi-GPU sharding); last = 0 means "to global_work_size".  Work-item ids, and
  * therefore seeds and output slots, stay global. */

@@ -70,6 +70,7 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB = 0, 1
+SCHED_TILES, SCHED_REGEN = 0, 1
 
 
 class Stats(ctypes.Structure):
@@ -94,6 +95,7 @@ _HIP_PROTOS = {
     "rtEnqueueCopyBufferToPointer": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
     "rtKernelSetMathMode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtKernelSetWorkRange": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
+    "rtKernelSetSchedule": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtKernelSetHitBuffers": (ctypes.c_int, [_vp, _vp, _vp]),
     "rtKernelSetStats": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtKernelSetTiming": (ctypes.c_int, [_vp, ctypes.c_int]),

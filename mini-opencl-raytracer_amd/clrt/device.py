@@ -137,6 +137,9 @@ class CLKernel:
     def set_math_mode(self, mode: int) -> None:
         check(self._lib.rtKernelSetMathMode(self.handle, int(mode)), "math mode")
 
+    def set_schedule(self, sched: int) -> None:
+        check(self._lib.rtKernelSetSchedule(self.handle, int(sched)), "schedule")
+
     def set_work_range(self, first: int, last: int) -> None:
         check(self._lib.rtKernelSetWorkRange(self.handle, int(first), int(last)), "work range")
 

@@ -67,6 +67,8 @@ struct rt_kernel_s {
     uint32_t u32[RT_ARG_COUNT] = {};  // slots 4..10 (raw 4-byte values)
     float f3[3][4] = {};              // slots 11..13
     int math = RT_MATH_PINNED;
+    int sched = RT_SCHED_REGEN;
+    uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
@@ -84,8 +86,8 @@ struct rt_kernel_s {
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[2][2][2] = {};  // [math][lds][stats] -> blocks per CU (0 = unknown)
-    size_t occ_smem[2][2][2] = {};
+    int occ_cache[2][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
+    size_t occ_smem[2][2][2][2] = {};
 };
 
 namespace {
@@ -318,6 +320,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, 4 * sizeof(unsigned long long), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
@@ -341,6 +344,7 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->packed_nodes) (void)hipFree(k->packed_nodes);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->dstats) (void)hipFree(k->dstats);
+    if (k->work_counter) (void)hipFree(k->work_counter);
     delete k;
     return RT_SUCCESS;
 }
@@ -411,11 +415,14 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.gidEnd = g1;
     const uint64_t row0 = g0 / W, row1 = (g1 + W - 1) / W;
     a.rowBegin = (uint32_t)row0;
-    a.tilesX = (W + 15) / 16;
-    const uint64_t tilesY = (row1 - row0 + 15) / 16;
+    a.rowCount = (uint32_t)(row1 - row0);
+    const uint32_t tile = k->sched == RT_SCHED_REGEN ? 8u : 16u;
+    a.tilesX = (W + tile - 1) / tile;
+    const uint64_t tilesY = (row1 - row0 + tile - 1) / tile;
     const uint64_t n_tiles = tilesY * a.tilesX;
-    if (n_tiles > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
+    if (n_tiles * 64 > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
+    a.workCounter = k->work_counter;
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
@@ -428,15 +435,20 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     k->last_lds = lds;
 
     const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;
-    int& occ = k->occ_cache[mi][lds][k->stats];
-    if (occ == 0 || k->occ_smem[mi][lds][k->stats] != smem) {
-        occ = rtk::occupancy_kernel_entry(k->math, lds, k->stats, smem);
-        k->occ_smem[mi][lds][k->stats] = smem;
+    const int si = k->sched == RT_SCHED_REGEN ? 1 : 0;
+    int& occ = k->occ_cache[si][mi][lds][k->stats];
+    if (occ == 0 || k->occ_smem[si][mi][lds][k->stats] != smem) {
+        occ = rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, smem);
+        k->occ_smem[si][mi][lds][k->stats] = smem;
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
     grid = std::min<uint64_t>(grid, n_tiles);
     if (grid == 0) grid = 1;
 
+    if (k->sched == RT_SCHED_REGEN) {
+        hipError_t me = hipMemsetAsync(k->work_counter, 0, 16, ctx->stream);
+        if (me != hipSuccess) return map_hip(me);
+    }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (k->timing) {
         ev0 = take_event(k);
@@ -444,7 +456,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
         if (!ev0 || !ev1) return RT_OUT_OF_RESOURCES;
         (void)hipEventRecord(ev0, ctx->stream);
     }
-    hipError_t e = rtk::launch_kernel_entry(a, k->math, lds, k->stats, (unsigned)grid, smem, ctx->stream);
+    hipError_t e = rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, ctx->stream);
     if (e != hipSuccess) return map_hip(e);
     if (k->timing) {
         (void)hipEventRecord(ev1, ctx->stream);
@@ -502,6 +514,13 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
     if (!k) return RT_INVALID_KERNEL;
     if (mode != RT_MATH_PINNED && mode != RT_MATH_DEVICELIB) return RT_INVALID_VALUE;
     k->math = mode;
+    return RT_SUCCESS;
+}
+
+int rtKernelSetSchedule(rt_kernel k, int sched) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN) return RT_INVALID_VALUE;
+    k->sched = sched;
     return RT_SUCCESS;
 }
 

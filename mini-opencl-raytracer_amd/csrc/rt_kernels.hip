@@ -272,6 +272,41 @@ struct LaneStats {
     uint32_t rays = 0, visits = 0, tests = 0, hits = 0;
 };
 
+// The body of Render's bounce loop after Intersect (kernel_bvh.cl:358-380): radiance and
+// beta updates, BRDF sample and the next ray.  Returns false where the reference breaks
+// out of the loop (miss, or pdf <= 0 / NaN).
+template <class M, bool kStats>
+__device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& radiance, F3& beta,
+                                             uint32_t& seed, const rt_cl_triangle* __restrict__ tris_full,
+                                             const rt_cl_material* __restrict__ mats, const KernelArgs& a,
+                                             LaneStats& st) {
+    if (h.prim < 0) {
+        radiance = radiance + beta * f3s(0.5f * a.skyboxIntensity);
+        return false;
+    }
+    if (kStats) ++st.hits;
+    // hit record of the last accepted triangle (kernel_bvh.cl:142-147)
+    const rt_cl_triangle& tri = tris_full[h.prim];
+    const float w = (1.0f - h.u) - h.v;
+    const F3 normal = normalize<M>((load3(tri.v2.normal) * h.u + load3(tri.v3.normal) * h.v) +
+                                   load3(tri.v1.normal) * w);
+    const F3 pos = ray.o + ray.d * h.t;
+    const rt_cl_material& mm = mats[tri.mtlIndex];
+    MatView m{load3(mm.diffuse), load3(mm.specular), load3(mm.emission), mm.roughness};
+
+    radiance = radiance + (beta * m.emission) * 50.0f;
+    F3 wi = f3s(0.0f);
+    float pdf = 0.0f;
+    const F3 f = sample_brdf<M>(-ray.d, wi, pdf, normal, m, seed);
+    if (pdf <= 0.0f || pdf != pdf) return false;
+    const F3 mul = (f * M::dot(wi, normal)) / pdf;
+    beta = beta * mul;
+    const float lp = light_pixel<M>(ray, h.t, normal, a.lightType);
+    radiance = radiance + (f3s(lp) * m.diffuse) * beta;
+    ray = init_ray<M>(pos + wi * 0.01f, wi);
+    return true;
+}
+
 // kernel_bvh.cl:349-384 (Render)
 template <class M, bool kStats>
 __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* __restrict__ tris_full,
@@ -287,32 +322,30 @@ __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* 
             prim_id = h.prim;
             prim_t = h.t;
         }
-        if (h.prim < 0) {
-            radiance = radiance + beta * f3s(0.5f * a.skyboxIntensity);
-            break;
-        }
-        if (kStats) ++st.hits;
-        // hit record of the last accepted triangle (kernel_bvh.cl:142-147)
-        const rt_cl_triangle& tri = tris_full[h.prim];
-        const float w = (1.0f - h.u) - h.v;
-        const F3 normal = normalize<M>((load3(tri.v2.normal) * h.u + load3(tri.v3.normal) * h.v) +
-                                       load3(tri.v1.normal) * w);
-        const F3 pos = ray.o + ray.d * h.t;
-        const rt_cl_material& mm = mats[tri.mtlIndex];
-        MatView m{load3(mm.diffuse), load3(mm.specular), load3(mm.emission), mm.roughness};
-
-        radiance = radiance + (beta * m.emission) * 50.0f;
-        F3 wi = f3s(0.0f);
-        float pdf = 0.0f;
-        const F3 f = sample_brdf<M>(-ray.d, wi, pdf, normal, m, seed);
-        if (pdf <= 0.0f || pdf != pdf) break;
-        const F3 mul = (f * M::dot(wi, normal)) / pdf;
-        beta = beta * mul;
-        const float lp = light_pixel<M>(ray, h.t, normal, a.lightType);
-        radiance = radiance + (f3s(lp) * m.diffuse) * beta;
-        ray = init_ray<M>(pos + wi * 0.01f, wi);
+        if (!shade_bounce<M, kStats>(h, ray, radiance, beta, seed, tris_full, mats, a, st)) break;
     }
     return F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
+}
+
+// kernel_bvh.cl:449-455: write (frameCount 0) or gamma-accumulate one work-item's result.
+template <class M>
+__device__ __forceinline__ void finish_pixel(const KernelArgs& a, uint32_t gid, F3 rad, int32_t pid,
+                                             float pt) {
+    F3 out;
+    if (a.frameCount == 0) {
+        out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
+    } else {
+        const float4 old = a.result[gid];
+        const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
+        const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
+        const F3 acc = ((lin * fm1) + rad) / fc;
+        out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+    }
+    a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
+    if (a.hitIds) {
+        a.hitIds[gid] = pid;
+        a.hitT[gid] = pt;
+    }
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
@@ -321,7 +354,18 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
     return x;
 }
 
-// ---- the kernel ---------------------------------------------------------------------------
+__device__ __forceinline__ void flush_stats(const KernelArgs& a, const LaneStats& st, int lane) {
+    const unsigned long long r = wave_sum(st.rays), v = wave_sum(st.visits), t = wave_sum(st.tests),
+                             h = wave_sum(st.hits);
+    if (lane == 0) {
+        atomicAdd(&a.stats[0], r);
+        atomicAdd(&a.stats[1], v);
+        atomicAdd(&a.stats[2], t);
+        atomicAdd(&a.stats[3], h);
+    }
+}
+
+// ---- the kernel (tile schedule) ------------------------------------------------------------
 template <class M, bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -371,34 +415,127 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
         int32_t pid = -1;
         float pt = 0.0f;
         const F3 rad = render<M, kStats>(sc, a.trisFull, a.materials, ray, seed, a, stack, pid, pt, st);
+        finish_pixel<M>(a, gid, rad, pid, pt);
+    }
+    if (kStats) flush_stats(a, st, lane);
+}
 
-        // kernel_bvh.cl:449-455
-        F3 out;
-        if (a.frameCount == 0) {
-            out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
-        } else {
-            const float4 old = a.result[gid];
-            const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
-            const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
-            const F3 acc = ((lin * fm1) + rad) / fc;
-            out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+// ---- path-regeneration schedule -------------------------------------------------------------
+// Same per-pixel computation, different scheduling: every lane of a persistent wave carries
+// one path; when a path ends (miss, pdf break, or lightBounces reached) the lane writes its
+// pixel and immediately starts the next pixel, taken from the wave's current 64-pixel chunk
+// (one 8x8 tile; one global atomic per chunk).  Lanes therefore stay busy across bounces
+// instead of idling until the longest path of their tile ends.  Every pixel still runs the
+// reference's exact sequence of operations with its own seed, so results are identical.
+template <class M, bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int tid = threadIdx.x;
+    const float4* nodes;
+    const float4* tris;
+    int* stack_base;
+    if (kLdsScene) {
+        float4* ln = smem;
+        float4* lt = smem + 2 * a.nNodes;
+        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
+        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+        nodes = ln;
+        tris = lt;
+        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
+        __syncthreads();
+    } else {
+        nodes = a.packedNodes;
+        tris = a.packedTris;
+        stack_base = reinterpret_cast<int*>(smem);
+    }
+    int* stack = stack_base + tid;
+    const SceneView sc{nodes, tris};
+
+    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
+    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
+    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
+    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
+    const uint32_t fh = frame_hash(a.frameCount);
+    const uint32_t bounces = (uint32_t)a.lightBounces;
+    const uint32_t total = a.nTiles * 64u;  // index space: 8x8-pixel tiles, tile-major
+    const uint32_t rowEnd = a.rowBegin + a.rowCount;
+    const int lane = tid & 63;
+
+    LaneStats st;
+    bool active = false;
+    uint32_t gid = 0, seed = 0, bounce = 0;
+    int32_t pid = -1;
+    float pt = 0.0f;
+    Ray ray{};
+    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
+    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    bool exhausted = false;                    // wave-uniform
+
+    for (;;) {
+        // ---- refill idle lanes from the wave's chunk --------------------------------------
+        while (!exhausted) {
+            const unsigned long long idle = __ballot(!active);
+            if (idle == 0ull) break;
+            if (chunk_used >= 64u) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(a.workCounter, 64u);
+                b = __shfl(b, 0, 64);
+                if (b >= total) {
+                    exhausted = true;
+                    break;
+                }
+                chunk_base = b;
+                chunk_used = 0;
+            }
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+            if (!active && rank < take) {
+                const uint32_t idx = chunk_base + chunk_used + rank;
+                const uint32_t tile = idx >> 6, w = idx & 63u;
+                const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+                const uint32_t x = tx * 8u + (w & 7u), row = a.rowBegin + ty * 8u + (w >> 3);
+                const uint64_t g64 = (uint64_t)row * a.width + x;
+                if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
+                    gid = (uint32_t)g64;
+                    seed = gid + fh;  // kernel_bvh.cl:445
+                    ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+                    radiance = f3s(0.0f);
+                    beta = f3s(1.0f);
+                    bounce = 0;
+                    pid = -1;
+                    pt = 0.0f;
+                    if (bounces > 0u) {
+                        active = true;
+                    } else {
+                        finish_pixel<M>(a, gid, f3s(0.0f), pid, pt);  // no bounce: radiance 0
+                    }
+                }
+            }
+            chunk_used += take;
         }
-        a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
-        if (a.hitIds) {
-            a.hitIds[gid] = pid;
-            a.hitT[gid] = pt;
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        // ---- one bounce of every live path -------------------------------------------------
+        if (active) {
+            if (kStats) ++st.rays;
+            const Traversal h = intersect<M, kStats>(sc, ray, stack, st.visits, st.tests);
+            if (bounce == 0u) {
+                pid = h.prim;
+                pt = h.t;
+            }
+            bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, a.trisFull, a.materials, a, st);
+            ++bounce;
+            if (!more || bounce >= bounces) {
+                const F3 rad{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
+                finish_pixel<M>(a, gid, rad, pid, pt);
+                active = false;
+            }
         }
     }
-    if (kStats) {
-        const unsigned long long r = wave_sum(st.rays), v = wave_sum(st.visits), t = wave_sum(st.tests),
-                       h = wave_sum(st.hits);
-        if (lane == 0) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[0]), (unsigned long long)r);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[1]), (unsigned long long)v);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[2]), (unsigned long long)t);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&a.stats[3]), (unsigned long long)h);
-        }
-    }
+    if (kStats) flush_stats(a, st, lane);
 }
 
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
@@ -427,40 +564,35 @@ __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restr
 // ---- host-side launch helpers ------------------------------------------------------------
 namespace rtk {
 
+// Kernel variants: [schedule][math][scene in LDS][stats].
+using KernelFn = void (*)(KernelArgs);
+
 template <class M, bool L, bool S>
-static hipError_t launch_one(const KernelArgs& a, unsigned grid, size_t smem, hipStream_t st) {
-    hipLaunchKernelGGL((kernel_entry<M, L, S>), dim3(grid), dim3(256), smem, st, a);
+static KernelFn pick_sched(int sched) {
+    return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
+}
+
+static KernelFn pick(int sched, int math, bool lds, bool stats) {
+    if (math == MathDeviceLib::kId) {
+        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched) : pick_sched<MathDeviceLib, true, false>(sched);
+        return stats ? pick_sched<MathDeviceLib, false, true>(sched) : pick_sched<MathDeviceLib, false, false>(sched);
+    }
+    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched) : pick_sched<MathPinned, true, false>(sched);
+    return stats ? pick_sched<MathPinned, false, true>(sched) : pick_sched<MathPinned, false, false>(sched);
+}
+
+hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
+                               size_t smem, hipStream_t st) {
+    KernelFn fn = pick(sched, math, lds, stats);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), smem, st, a);
     return hipGetLastError();
 }
 
-template <class M, bool L, bool S>
-static int occupancy_one(size_t smem) {
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel_entry<M, L, S>, 256, smem) !=
-        hipSuccess)
-        return 1;
+    KernelFn fn = pick(sched, math, lds, stats);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, smem) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
-}
-
-hipError_t launch_kernel_entry(const KernelArgs& a, int math, bool lds, bool stats, unsigned grid,
-                               size_t smem, hipStream_t st) {
-#define RTK_DISPATCH(MM)                                                           \
-    if (lds) return stats ? launch_one<MM, true, true>(a, grid, smem, st)          \
-                          : launch_one<MM, true, false>(a, grid, smem, st);        \
-    return stats ? launch_one<MM, false, true>(a, grid, smem, st)                  \
-                 : launch_one<MM, false, false>(a, grid, smem, st);
-    if (math == MathDeviceLib::kId) { RTK_DISPATCH(MathDeviceLib) }
-    RTK_DISPATCH(MathPinned)
-#undef RTK_DISPATCH
-}
-
-int occupancy_kernel_entry(int math, bool lds, bool stats, size_t smem) {
-#define RTK_OCC(MM)                                                                        \
-    if (lds) return stats ? occupancy_one<MM, true, true>(smem) : occupancy_one<MM, true, false>(smem); \
-    return stats ? occupancy_one<MM, false, true>(smem) : occupancy_one<MM, false, false>(smem);
-    if (math == MathDeviceLib::kId) { RTK_OCC(MathDeviceLib) }
-    RTK_OCC(MathPinned)
-#undef RTK_OCC
 }
 
 hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,

@@ -24,16 +24,20 @@ struct KernelArgs {
     float camPos[3], camFront[3], camUp[3];  // slots 11-13 (w ignored)
     // work decomposition: work-items [gidBegin, gidEnd), rows [rowBegin, rowEnd)
     uint64_t gidBegin, gidEnd;
-    uint32_t rowBegin, tilesX, nTiles;
+    uint32_t rowBegin, rowCount, tilesX, nTiles;  // tiles: 16x16 (tile schedule) or 8x8 (regen)
+    uint32_t* workCounter;              // regen schedule: next 64-pixel chunk (zeroed per launch)
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
     unsigned long long* stats;          // [rays, node visits, triangle tests, hits]
 };
 
-hipError_t launch_kernel_entry(const KernelArgs& a, int math, bool lds, bool stats, unsigned grid,
+constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
+constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
+
+hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);
-int occupancy_kernel_entry(int math, bool lds, bool stats, size_t smem);
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
 hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
                        const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, hipStream_t st);
 

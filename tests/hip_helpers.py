@@ -11,7 +11,7 @@ class HipRenderer:
     """One context + kernel + scene + output buffer; frames rendered on demand."""
 
     def __init__(self, scene, width, height, math=N.MATH_PINNED, device=0, hits=False,
-                 stats=False, force_global=False, global_size=None):
+                 stats=False, force_global=False, global_size=None, sched=N.SCHED_REGEN):
         self.W, self.H = width, height
         self.n = global_size if global_size is not None else width * height
         self.ctx = clrt.CLContext(device)
@@ -27,6 +27,7 @@ class HipRenderer:
         self.k.set_int(N.WIDTH, width)
         self.k.set_int(N.HEIGHT, height)
         self.k.set_math_mode(math)
+        self.k.set_schedule(sched)
         self.k.force_global_scene(force_global)
         self.k.set_stats(stats)
         self.hit_bufs = None

@@ -112,6 +112,31 @@ def test_frame_count_zero_path(cornell, oracle_mod):
     _assert_bits(rgb(got), rgb(want), "frame 0")
 
 
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB])
+def test_schedules_agree_bit_exact(cornell, math):
+    """Tile schedule and path-regeneration schedule compute identical pixels and counters."""
+    outs = []
+    for sched in (N.SCHED_TILES, N.SCHED_REGEN):
+        r = HipRenderer(cornell, 301, 157, math=math, hits=True, stats=True, sched=sched)
+        for f in (1, 2, 3):
+            r.frame(f, light_bounces=9)
+        outs.append((r.result(), r.hits(), r.k.stats()))
+        r.close()
+    _assert_bits(outs[0][0], outs[1][0], "tiles vs regen")
+    assert np.array_equal(outs[0][1][0], outs[1][1][0])
+    for key in ("rays", "node_visits", "tri_tests", "hits"):
+        assert outs[0][2][key] == outs[1][2][key], key
+
+
+def test_zero_bounces_writes_black(cornell, oracle_mod):
+    r = HipRenderer(cornell, 64, 48)
+    r.frame(1, light_bounces=0)
+    got = r.result()
+    r.close()
+    want, _, _, _ = _oracle(oracle_mod, cornell, 64, 48, [1], 0)
+    _assert_bits(rgb(got), rgb(want), "0 bounces")
+
+
 def test_global_scene_path_equals_lds_path(cornell):
     outs = []
     for force in (False, True):
