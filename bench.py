@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--bounces", type=int, default=9)
     p.add_argument("--math", choices=["pinned", "devicelib"], default="pinned")
-    p.add_argument("--sched", choices=["regen", "tiles"], default="regen")
+    p.add_argument("--sched", choices=["regen", "tiles", "step"], default="step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     return p.parse_args()
@@ -88,7 +88,7 @@ class Rank:
         k.set_float3(N.CAMERA_FRONT, CAMERA[1])
         k.set_float3(N.CAMERA_UP, CAMERA[2])
         k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
-        k.set_schedule(N.SCHED_TILES if args.sched == "tiles" else N.SCHED_REGEN)
+        k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP}[args.sched])
         k.set_work_range(self.row0 * W, self.row1 * W)
 
     def render(self):

@@ -108,11 +108,15 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset
 int rtKernelSetMathMode(rt_kernel k, int mode);
 
 /* Work schedule of the kernel (same results, different lane scheduling):
- * RT_SCHED_REGEN (default) -- persistent lanes; a lane whose path ends starts the next
+ * RT_SCHED_REGEN           -- persistent lanes; a lane whose path ends starts the next
  *                             pixel of its wave's 8x8 chunk (path regeneration);
- * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles). */
+ * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles);
+ * RT_SCHED_STEP (default)  -- per-wave state machine: every step advances each lane by one
+ *                             BVH node or one triangle; shading and pixel refill run when
+ *                             enough lanes are ready. */
 #define RT_SCHED_TILES 0
 #define RT_SCHED_REGEN 1
+#define RT_SCHED_STEP 2
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
 /* Restrict the next launches to work-items [first, last) (pixel-row tiles for
@@ -130,6 +134,9 @@ typedef struct rt_stats {
     uint64_t rays, node_visits, tri_tests, hits;
     uint64_t launches;
     double kernel_ms;  /* sum of KernelEntry durations (HIP events) when timing is on */
+    /* diagnostic (step schedule, stats on): shader-clock cycles summed over waves spent
+     * refilling/finishing pixels, traversing, shading, and in total */
+    uint64_t cycles_refill, cycles_traverse, cycles_shade, cycles_total;
 } rt_stats;
 int rtKernelSetStats(rt_kernel k, int enable);
 int rtKernelSetTiming(rt_kernel k, int enable);

@@ -70,13 +70,15 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB = 0, 1
-SCHED_TILES, SCHED_REGEN = 0, 1
+SCHED_TILES, SCHED_REGEN, SCHED_STEP = 0, 1, 2
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
                 ("tri_tests", ctypes.c_uint64), ("hits", ctypes.c_uint64),
-                ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
+                ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
+                ("cycles_refill", ctypes.c_uint64), ("cycles_traverse", ctypes.c_uint64),
+                ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64)]
 
 
 _vp = ctypes.c_void_p

@@ -166,7 +166,9 @@ class CLKernel:
         s = N.Stats()
         check(self._lib.rtKernelGetStats(self.handle, ctypes.byref(s)), "stats")
         return {"rays": s.rays, "node_visits": s.node_visits, "tri_tests": s.tri_tests,
-                "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms}
+                "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms,
+                "cycles": {"refill": s.cycles_refill, "traverse": s.cycles_traverse,
+                           "shade": s.cycles_shade, "total": s.cycles_total}}
 
     def reset_stats(self) -> None:
         check(self._lib.rtKernelResetStats(self.handle), "reset stats")

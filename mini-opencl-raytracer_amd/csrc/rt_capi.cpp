@@ -28,6 +28,7 @@ namespace {
 
 constexpr uint64_t kKnownFlags =
     RT_MEM_READ_WRITE | RT_MEM_WRITE_ONLY | RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
+constexpr int kStatWords = 8;                 // rt_stats counters kept on the device
 constexpr int kMaxStack = 64;                  // nodesToVisit[64], kernel_bvh.cl:181
 constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
 
@@ -67,7 +68,7 @@ struct rt_kernel_s {
     uint32_t u32[RT_ARG_COUNT] = {};  // slots 4..10 (raw 4-byte values)
     float f3[3][4] = {};              // slots 11..13
     int math = RT_MATH_PINNED;
-    int sched = RT_SCHED_REGEN;
+    int sched = RT_SCHED_STEP;
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
@@ -86,8 +87,8 @@ struct rt_kernel_s {
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[2][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
-    size_t occ_smem[2][2][2][2] = {};
+    int occ_cache[3][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
+    size_t occ_smem[3][2][2][2] = {};
 };
 
 namespace {
@@ -319,9 +320,9 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     rt_kernel k = new (std::nothrow) rt_kernel_s();
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
-    hipError_t e = hipMalloc(&k->dstats, 4 * sizeof(unsigned long long));
+    hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
-    if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, 4 * sizeof(unsigned long long), ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
         delete k;
@@ -416,7 +417,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     const uint64_t row0 = g0 / W, row1 = (g1 + W - 1) / W;
     a.rowBegin = (uint32_t)row0;
     a.rowCount = (uint32_t)(row1 - row0);
-    const uint32_t tile = k->sched == RT_SCHED_REGEN ? 8u : 16u;
+    const uint32_t tile = k->sched == RT_SCHED_TILES ? 16u : 8u;
     a.tilesX = (W + tile - 1) / tile;
     const uint64_t tilesY = (row1 - row0 + tile - 1) / tile;
     const uint64_t n_tiles = tilesY * a.tilesX;
@@ -435,7 +436,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     k->last_lds = lds;
 
     const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;
-    const int si = k->sched == RT_SCHED_REGEN ? 1 : 0;
+    const int si = k->sched;
     int& occ = k->occ_cache[si][mi][lds][k->stats];
     if (occ == 0 || k->occ_smem[si][mi][lds][k->stats] != smem) {
         occ = rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, smem);
@@ -445,7 +446,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     grid = std::min<uint64_t>(grid, n_tiles);
     if (grid == 0) grid = 1;
 
-    if (k->sched == RT_SCHED_REGEN) {
+    if (k->sched != RT_SCHED_TILES) {
         hipError_t me = hipMemsetAsync(k->work_counter, 0, 16, ctx->stream);
         if (me != hipSuccess) return map_hip(me);
     }
@@ -519,7 +520,7 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
 
 int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (!k) return RT_INVALID_KERNEL;
-    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN) return RT_INVALID_VALUE;
+    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP) return RT_INVALID_VALUE;
     k->sched = sched;
     return RT_SUCCESS;
 }
@@ -557,7 +558,7 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     if (!k || !out) return RT_INVALID_VALUE;
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[kStatWords] = {};
     hipError_t e = hipMemcpyAsync(h, k->dstats, sizeof(h), hipMemcpyDeviceToHost, k->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
     if (e != hipSuccess) return map_hip(e);
@@ -567,6 +568,10 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     out->node_visits = h[1];
     out->tri_tests = h[2];
     out->hits = h[3];
+    out->cycles_refill = h[4];
+    out->cycles_traverse = h[5];
+    out->cycles_shade = h[6];
+    out->cycles_total = h[7];
     out->launches = k->launches;
     out->kernel_ms = k->kernel_ms;
     return RT_SUCCESS;
@@ -580,7 +585,7 @@ int rtKernelResetStats(rt_kernel k) {
     if (rc) return rc;
     k->launches = 0;
     k->kernel_ms = 0.0;
-    hipError_t e = hipMemsetAsync(k->dstats, 0, 4 * sizeof(unsigned long long), k->ctx->stream);
+    hipError_t e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), k->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
     return map_hip(e);
 }

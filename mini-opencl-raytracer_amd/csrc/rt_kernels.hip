@@ -191,32 +191,6 @@ __device__ __forceinline__ void onb(F3 n, F3& s, F3& t) {
     s = M::cross(n, t);
 }
 
-template <class M>
-__device__ __forceinline__ F3 sample_hemisphere_cosine(F3 n, uint32_t& seed) {
-    const float phi = kTwoPi * next_rand(seed);
-    const float s2 = next_rand(seed);
-    const float sinT = __builtin_sqrtf(s2);
-    F3 s, t;
-    onb<M>(n, s, t);
-    const F3 a = (s * M::cos(phi)) * sinT;
-    const F3 b = (t * M::sin(phi)) * sinT;
-    return normalize<M>((a + b) + n * __builtin_sqrtf(1.0f - s2));
-}
-
-template <class M>
-__device__ __forceinline__ F3 sample_ggx(F3 n, float alpha, float& cosTheta, uint32_t& seed) {
-    const float phi = kTwoPi * next_rand(seed);
-    (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
-    const float r = next_rand(seed);
-    cosTheta = M::pow(r, 1.0f / (alpha + 1.0f));
-    const float sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - cosTheta * cosTheta));
-    F3 s, t;
-    onb<M>(n, s, t);
-    const F3 a = (s * M::cos(phi)) * sinT;
-    const F3 b = (t * M::sin(phi)) * sinT;
-    return normalize<M>((a + b) + n * cosTheta);
-}
-
 struct MatView {
     F3 diffuse, specular, emission;
     float roughness;
@@ -224,13 +198,37 @@ struct MatView {
 
 // SampleBrdf (kernel_bvh.cl:294-302) with SampleSpecular (:271-292) and SampleDiffuse
 // (:264-269).  G and F of SampleSpecular are dead in the reference and not evaluated.
+//
+// SampleGGX (:227-239) and SampleHemisphereCosine (:79-90) end in the same expression,
+// normalize((s*cos(phi))*sinT + (t*sin(phi))*sinT + n*c), with c = cosTheta (GGX) or
+// sqrt(1 - sinThetaSqr) (cosine).  The lane-specific scalars are drawn in a short branch
+// and the expensive tail (frame, sin, cos, normalize) is executed once for both kinds of
+// lanes -- each lane still performs exactly the reference's operations, in its order.
 template <class M>
 __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const MatView& m,
                                           uint32_t& seed) {
-    if (next_rand(seed) > 0.5f) {
-        float cosTheta = 1.0f;
-        const float alpha = 2.0f / M::pow2(m.roughness) - 2.0f;
-        const F3 wh = sample_ggx<M>(n, alpha, cosTheta, seed);
+    const bool spec = next_rand(seed) > 0.5f;
+    const float phi = kTwoPi * next_rand(seed);
+    float alpha = 0.0f, sinT, c;
+    if (spec) {
+        alpha = 2.0f / M::pow2(m.roughness) - 2.0f;
+        (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
+        const float r = next_rand(seed);
+        c = M::pow(r, 1.0f / (alpha + 1.0f));  // cosTheta
+        sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - c * c));
+    } else {
+        const float s2 = next_rand(seed);
+        sinT = __builtin_sqrtf(s2);
+        c = __builtin_sqrtf(1.0f - s2);
+    }
+    F3 s, t;
+    onb<M>(n, s, t);
+    const F3 pa = (s * M::cos(phi)) * sinT;
+    const F3 pb = (t * M::sin(phi)) * sinT;
+    const F3 dir = normalize<M>((pa + pb) + n * c);
+    if (spec) {
+        const F3 wh = dir;
+        const float cosTheta = c;
         wi = (-wo) + wh * (2.0f * M::dot(wo, wh));
         if (M::dot(wi, n) * M::dot(wo, n) < 0.000001f) return f3s(0.0f);
         const float a2 = alpha * alpha;
@@ -240,7 +238,7 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
             (4.0f * M::max(M::dot(wi, n), 0.0f)) * M::max(M::dot(wo, n), 0.0f) + 0.001f;
         return m.specular * (D / denom);
     }
-    wi = sample_hemisphere_cosine<M>(n, seed);
+    wi = dir;
     pdf = M::dot(wi, n) * kInvPi;
     return m.diffuse * kInvPi;
 }
@@ -538,6 +536,220 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
     if (kStats) flush_stats(a, st, lane);
 }
 
+// ---- step schedule: a per-wave state machine ------------------------------------------------
+// Every lane is in one of four states:
+//   IDLE  -- no path; refilled (new pixel -> camera ray) when enough lanes are idle
+//   TRAV  -- at BVH node `cur`: one RayBounds per step (kernel_bvh.cl:184-215)
+//   LEAF  -- inside a passing leaf: ONE RayTriangle per step, in the leaf's order
+//   SHADE -- traversal finished; shaded when enough lanes are ready (kernel_bvh.cl:358-380)
+//   DONE  -- path finished; its pixel is accumulated (kernel_bvh.cl:449-455) together with
+//            the refill, so that code also runs with many lanes
+// Each step advances every TRAV/LEAF lane by one node or one triangle, so a wave no longer
+// runs a 4-triangle leaf loop for the few lanes that happen to sit at a leaf, and the heavy
+// per-bounce (shading) and per-path (accumulate + next camera ray) code runs with many lanes
+// at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
+// t, hit and pixel -- is exactly the reference's.
+constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
+constexpr uint32_t kRefillMin = 24;  // finish + refill when at least this many lanes are free
+constexpr uint32_t kShadeMin = 24;   // shade when at least this many lanes are ready
+
+__device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
+
+template <class M, bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) void kernel_entry_step(KernelArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int tid = threadIdx.x;
+    const float4* nodes;
+    const float4* tris;
+    int* stack_base;
+    if (kLdsScene) {
+        float4* ln = smem;
+        float4* lt = smem + 2 * a.nNodes;
+        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
+        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+        nodes = ln;
+        tris = lt;
+        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
+        __syncthreads();
+    } else {
+        nodes = a.packedNodes;
+        tris = a.packedTris;
+        stack_base = reinterpret_cast<int*>(smem);
+    }
+    int* stack = stack_base + tid;
+
+    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
+    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
+    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
+    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
+    const uint32_t fh = frame_hash(a.frameCount);
+    const uint32_t bounces = (uint32_t)a.lightBounces;
+    const uint32_t total = a.nTiles * 64u;
+    const uint32_t rowEnd = a.rowBegin + a.rowCount;
+    const int lane = tid & 63;
+
+    LaneStats st;
+    uint32_t state = kIdle;
+    uint32_t gid = 0, seed = 0, bounce = 0;
+    int32_t pid = -1;
+    float pt = 0.0f;
+    Ray ray{};
+    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
+    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
+    int sp = 0, cur = 0;
+    uint32_t leaf_i = 0, leaf_end = 0;
+    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    bool exhausted = false;                    // wave-uniform
+    // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
+    uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
+    const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
+
+    for (;;) {
+        // ---- finish + refill: accumulate finished paths, start new pixels ----------------------
+        uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t n_free = popc_ballot(state == kIdle || state == kDone);
+        if (n_free == 64u || (!exhausted && n_free >= kRefillMin)) {
+            if (state == kDone) {
+                finish_pixel<M>(a, gid, radiance, pid, pt);
+                state = kIdle;
+            }
+            while (!exhausted) {
+                const unsigned long long idle = __ballot(state == kIdle);
+                if (idle == 0ull) break;
+                if (chunk_used >= 64u) {
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(a.workCounter, 64u);
+                    b = __shfl(b, 0, 64);
+                    if (b >= total) {
+                        exhausted = true;
+                        break;
+                    }
+                    chunk_base = b;
+                    chunk_used = 0;
+                }
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+                if (state == kIdle && rank < take) {
+                    const uint32_t idx = chunk_base + chunk_used + rank;
+                    const uint32_t tile = idx >> 6, w = idx & 63u;
+                    const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+                    const uint32_t x = tx * 8u + (w & 7u), row = a.rowBegin + ty * 8u + (w >> 3);
+                    const uint64_t g64 = (uint64_t)row * a.width + x;
+                    if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
+                        gid = (uint32_t)g64;
+                        seed = gid + fh;  // kernel_bvh.cl:445
+                        ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+                        radiance = f3s(0.0f);
+                        beta = f3s(1.0f);
+                        bounce = 0;
+                        pid = -1;
+                        pt = 0.0f;
+                        if (bounces > 0u) {
+                            state = kTrav;
+                            h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                            sp = 0;
+                            cur = 0;
+                            if (kStats) ++st.rays;
+                        } else {
+                            state = kDone;  // no bounce: radiance max(0, 0) = 0
+                        }
+                    }
+                }
+                chunk_used += take;
+            }
+        }
+        uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
+        if (kStats) cyc_refill += tB - tA;
+        {
+            const uint32_t n_idle = popc_ballot(state == kIdle);
+            if (n_idle == 64u) {
+                if (exhausted) break;
+                continue;
+            }
+        }
+
+        // ---- traversal steps -----------------------------------------------------------------
+        for (;;) {
+            const unsigned long long busy = __ballot(state == kTrav || state == kLeaf);
+            if (busy == 0ull) break;
+            if (popc_ballot(state == kShade) >= kShadeMin) break;
+            if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
+            bool pop = false;
+            if (state == kTrav) {
+                const float4 q0 = nodes[2 * cur];
+                const float4 q1 = nodes[2 * cur + 1];
+                if (kStats) ++st.visits;
+                pop = true;
+                if (ray_bounds(q0, q1, ray, h.t)) {
+                    const uint32_t off = __float_as_uint(q1.z);
+                    const uint32_t meta = __float_as_uint(q1.w);
+                    const uint32_t np = meta & 0xffffu;
+                    if (np > 0) {
+                        state = kLeaf;
+                        leaf_i = off;
+                        leaf_end = off + np;
+                        pop = false;
+                    } else {
+                        const uint32_t axis = meta >> 16;
+                        const bool far_first = (ray.sgn >> axis) & 1u;
+                        stack[sp * 256] = far_first ? cur + 1 : (int)off;
+                        ++sp;
+                        cur = far_first ? (int)off : cur + 1;
+                        pop = false;
+                    }
+                }
+            } else if (state == kLeaf) {
+                if (kStats) ++st.tests;
+                ray_triangle<M>(tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                ++leaf_i;
+                pop = leaf_i == leaf_end;
+            }
+            if (pop) {
+                if (sp == 0) {
+                    state = kShade;
+                } else {
+                    --sp;
+                    cur = stack[sp * 256];
+                    state = kTrav;
+                }
+            }
+        }
+
+        // ---- shading ---------------------------------------------------------------------------
+        uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
+        if (kStats) cyc_trav += tC - tB;
+        if (state == kShade) {
+            if (bounce == 0u) {
+                pid = h.prim;
+                pt = h.t;
+            }
+            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, a.trisFull, a.materials, a, st);
+            ++bounce;
+            if (!more || bounce >= bounces) {
+                radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
+                state = kDone;
+            } else {
+                state = kTrav;
+                h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                sp = 0;
+                cur = 0;
+                if (kStats) ++st.rays;
+            }
+        }
+        if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tC;
+    }
+    if (kStats) {
+        flush_stats(a, st, lane);
+        if (lane == 0) {
+            atomicAdd(&a.stats[4], (unsigned long long)cyc_refill);
+            atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
+            atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
+            atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
+        }
+    }
+}
+
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
 __global__ void pack_nodes(const rt_cl_bvh_node* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -569,6 +781,7 @@ using KernelFn = void (*)(KernelArgs);
 
 template <class M, bool L, bool S>
 static KernelFn pick_sched(int sched) {
+    if (sched == kSchedStep) return kernel_entry_step<M, L, S>;
     return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
 }
 

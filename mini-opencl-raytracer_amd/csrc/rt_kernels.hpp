@@ -29,11 +29,12 @@ struct KernelArgs {
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
-    unsigned long long* stats;          // [rays, node visits, triangle tests, hits]
+    unsigned long long* stats;          // [rays, node visits, triangle tests, hits, 4 phase-cycle sums]
 };
 
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
 constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
+constexpr int kSchedStep = 2;   // per-wave state machine: node / triangle steps, batched shading
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);

@@ -29,11 +29,15 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchdl) run bench_devicelib 600 python bench.py --math devicelib --no-cpu-baseline ;;
+    benchstep) run bench_pin_step 600 python bench.py --sched step --no-cpu-baseline && \
+             run bench_dl_step 600 python bench.py --math devicelib --sched step --no-cpu-baseline && \
+             run bench_dl_regen 600 python bench.py --math devicelib --sched regen --no-cpu-baseline ;;
     benchab) run bench_pin_tiles 600 python bench.py --sched tiles --no-cpu-baseline && \
              run bench_pin_regen 600 python bench.py --sched regen --no-cpu-baseline && \
              run bench_dl_tiles 600 python bench.py --math devicelib --sched tiles --no-cpu-baseline && \
              run bench_dl_regen 600 python bench.py --math devicelib --sched regen --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    phase) run phase 300 python scripts/phase_profile.py ;;
     refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline && \
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;

@@ -11,7 +11,7 @@ class HipRenderer:
     """One context + kernel + scene + output buffer; frames rendered on demand."""
 
     def __init__(self, scene, width, height, math=N.MATH_PINNED, device=0, hits=False,
-                 stats=False, force_global=False, global_size=None, sched=N.SCHED_REGEN):
+                 stats=False, force_global=False, global_size=None, sched=N.SCHED_STEP):
         self.W, self.H = width, height
         self.n = global_size if global_size is not None else width * height
         self.ctx = clrt.CLContext(device)

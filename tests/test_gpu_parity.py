@@ -116,16 +116,17 @@ def test_frame_count_zero_path(cornell, oracle_mod):
 def test_schedules_agree_bit_exact(cornell, math):
     """Tile schedule and path-regeneration schedule compute identical pixels and counters."""
     outs = []
-    for sched in (N.SCHED_TILES, N.SCHED_REGEN):
+    for sched in (N.SCHED_TILES, N.SCHED_REGEN, N.SCHED_STEP):
         r = HipRenderer(cornell, 301, 157, math=math, hits=True, stats=True, sched=sched)
         for f in (1, 2, 3):
             r.frame(f, light_bounces=9)
         outs.append((r.result(), r.hits(), r.k.stats()))
         r.close()
-    _assert_bits(outs[0][0], outs[1][0], "tiles vs regen")
-    assert np.array_equal(outs[0][1][0], outs[1][1][0])
-    for key in ("rays", "node_visits", "tri_tests", "hits"):
-        assert outs[0][2][key] == outs[1][2][key], key
+    for o in outs[1:]:
+        _assert_bits(outs[0][0], o[0], "schedules")
+        assert np.array_equal(outs[0][1][0], o[1][0])
+        for key in ("rays", "node_visits", "tri_tests", "hits"):
+            assert outs[0][2][key] == o[2][key], key
 
 
 def test_zero_bounces_writes_black(cornell, oracle_mod):
