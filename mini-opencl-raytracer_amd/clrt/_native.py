@@ -13,7 +13,7 @@ import numpy as np
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(_PKG_ROOT, "lib")
-HIP_LIB_PATH = os.path.join(LIB_DIR, "librt_hip.so")
+HIP_LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(LIB_DIR, "librt_hip.so")
 SCENE_LIB_PATH = os.path.join(LIB_DIR, "librt_scene.so")
 
 # ---- status codes (include/rt_status.h == cl_int codes, CLutils.h:31-105) -------------

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -69,6 +70,7 @@ struct rt_kernel_s {
     float f3[3][4] = {};              // slots 11..13
     int math = RT_MATH_PINNED;
     int sched = RT_SCHED_STEP;
+    uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
@@ -320,6 +322,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     rt_kernel k = new (std::nothrow) rt_kernel_s();
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
+    if (const char* v = std::getenv("RT_REFILL_MIN")) k->refill_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
@@ -424,6 +428,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     if (n_tiles * 64 > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
     a.workCounter = k->work_counter;
+    a.refillMin = k->refill_min;
+    a.shadeMin = k->shade_min;
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;

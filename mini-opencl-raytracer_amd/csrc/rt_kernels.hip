@@ -550,13 +550,17 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
 // at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
-constexpr uint32_t kRefillMin = 24;  // finish + refill when at least this many lanes are free
-constexpr uint32_t kShadeMin = 24;   // shade when at least this many lanes are ready
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
+#ifdef RT_STEP_WAVES_PER_EU
+#define RT_STEP_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_WAVES_PER_EU, 8)))
+#else
+#define RT_STEP_OCC
+#endif
+
 template <class M, bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) void kernel_entry_step(KernelArgs a) {
+__global__ __launch_bounds__(256) RT_STEP_OCC void kernel_entry_step(KernelArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
     const float4* nodes;
@@ -587,6 +591,8 @@ __global__ __launch_bounds__(256) void kernel_entry_step(KernelArgs a) {
     const uint32_t total = a.nTiles * 64u;
     const uint32_t rowEnd = a.rowBegin + a.rowCount;
     const int lane = tid & 63;
+    const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
+    const uint32_t kShadeMin = a.shadeMin;    // shade when this many lanes are ready
 
     LaneStats st;
     uint32_t state = kIdle;

@@ -26,6 +26,7 @@ struct KernelArgs {
     uint64_t gidBegin, gidEnd;
     uint32_t rowBegin, rowCount, tilesX, nTiles;  // tiles: 16x16 (tile schedule) or 8x8 (regen)
     uint32_t* workCounter;              // regen schedule: next 64-pixel chunk (zeroed per launch)
+    uint32_t refillMin, shadeMin;       // step schedule batching thresholds (lanes)
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
