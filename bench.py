@@ -35,6 +35,7 @@ sys.path.insert(0, os.path.join(REPO, "mini-opencl-raytracer_amd"))
 
 import clrt  # noqa: E402
 from clrt import _native as N  # noqa: E402
+from clrt import multigpu as mg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
 CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
@@ -57,16 +58,16 @@ def parse():
 
 
 class Rank:
-    """One GPU's share of the image: rows [row0, row1) as work-items [row0*W, row1*W)."""
+    """One GPU's share of the image: the interleaved 8-row bands b % world == rank
+    (clrt.multigpu), rendered at their global positions (global seeds)."""
 
     def __init__(self, scene, args, device, rank, world):
         self.args = args
         W, H = args.width, args.height
         self.W, self.H = W, H
-        rows = (H + world - 1) // world
-        self.rows_per_rank = rows
-        self.row0 = min(H, rank * rows)
-        self.row1 = min(H, self.row0 + rows)
+        self.rank, self.world = rank, world
+        self.bands = mg.rank_bands(H, world, rank)
+        self.pixels = sum(min(H, (b + 1) * mg.BAND_ROWS) - b * mg.BAND_ROWS for b in self.bands) * W
         self.ctx = clrt.CLContext(device)
         self.k = clrt.CLKernel(self.ctx, "KernelEntry")
         flags = N.MEM_READ_ONLY | N.MEM_COPY_HOST_PTR
@@ -89,7 +90,7 @@ class Rank:
         k.set_float3(N.CAMERA_UP, CAMERA[2])
         k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
         k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP}[args.sched])
-        k.set_work_range(self.row0 * W, self.row1 * W)
+        k.set_row_interleave(world, rank)
 
     def render(self):
         """frames 1..F accumulated (RenderFrame's m_FrameCount sequence)."""
@@ -154,18 +155,20 @@ def main():
     gather = None
     if dist is not None:
         import torch
-        tile_bytes = r.rows_per_rank * r.W * 16
-        tile = torch.empty(tile_bytes // 4, dtype=torch.float32, device=f"cuda:{local}")
-        full = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
+        stage = torch.empty(mg.staging_bytes(r.W, r.H, world) // 4, dtype=torch.float32, device=f"cuda:{local}")
+        plans = [mg.pack_plan(r.W, r.H, world, q) for q in range(world)]
 
         def gather():
-            # this rank's rows -> staging tensor (device to device on the kernel's stream),
-            # then gather of the row tiles to rank 0 over RCCL (grouped send/recv)
-            n = (r.row1 - r.row0) * r.W * 16
-            if n:
-                r.ctx.CopyToDevicePointer(r.out, r.row0 * r.W * 16, n, tile.data_ptr())
+            # pack this rank's bands (2-D device copy on the kernel's stream), gather the
+            # staging buffers to rank 0 over RCCL, unpack them into rank 0's image
+            mg.pack_device(r.ctx, r.out, plans[rank], stage.data_ptr())
+            r.finish()
+            parts = mg.gather_to_root(dist, stage, rank, world)
+            if rank == 0:
+                torch.cuda.current_stream().synchronize()
+                for q in range(1, world):
+                    mg.unpack_device(r.ctx, parts[q].data_ptr(), plans[q], r.out)
                 r.finish()
-            dist.gather(tile, full, dst=0)
 
         tot = torch.tensor(counts, dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tot)
@@ -211,7 +214,7 @@ def main():
     launches = max(1, ks["launches"])
     kernel_ms = ks["kernel_ms"] / launches
     local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
-    tile_px = (r.row1 - r.row0) * r.W
+    tile_px = r.pixels
     alg_bytes = (48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames + 32 * tile_px
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     traffic = None
@@ -245,7 +248,7 @@ def main():
         "data": "reference scene cornell.obj (scenes/cornell_scene.npz); rays generated in-kernel",
         "config": {"workload": f"cornell {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "schedule": args.sched, "parallelism": f"row tiles x{world}" + (" + RCCL gather" if world > 1 else ""),
+                   "math": args.math, "schedule": args.sched, "parallelism": f"interleaved 8-row bands x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

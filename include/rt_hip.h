@@ -124,6 +124,18 @@ int rtKernelSetSchedule(rt_kernel k, int sched);
  * therefore seeds and output slots, stay global. */
 int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last);
 
+/* Interleaved 8-row bands for load-balanced multi-GPU sharding: the next launches render
+ * only the bands b (rows 8b..8b+7 of the work range) with b % period == phase.  (1, 0)
+ * = every band.  Not available with RT_SCHED_TILES (RT_INVALID_OPERATION at launch). */
+int rtKernelSetRowInterleave(rt_kernel k, unsigned period, unsigned phase);
+
+/* 2-D device copies for packing / unpacking band-interleaved tiles around a collective:
+ * `rows` rows of `width_bytes`, source and destination row pitches in bytes. */
+int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offset, size_t src_pitch,
+                                     size_t width_bytes, size_t rows, void* dst_device, size_t dst_pitch);
+int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src_device, size_t src_pitch, rt_mem dst,
+                                     size_t dst_offset, size_t dst_pitch, size_t width_bytes, size_t rows);
+
 /* Primary-ray outputs per work-item: hit primitive index into the BVH-ordered triangle
  * array (-1 = miss) and isect.t.  Pass NULL to disable. Buffers need 4 B per work-item. */
 int rtKernelSetHitBuffers(rt_kernel k, rt_mem hit_ids, rt_mem hit_t);

@@ -98,6 +98,11 @@ _HIP_PROTOS = {
     "rtKernelSetMathMode": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtKernelSetWorkRange": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
     "rtKernelSetSchedule": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtKernelSetRowInterleave": (ctypes.c_int, [_vp, ctypes.c_uint, ctypes.c_uint]),
+    "rtEnqueueCopyBufferRectToPointer": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                                        ctypes.c_size_t, _vp, ctypes.c_size_t]),
+    "rtEnqueueCopyPointerRectToBuffer": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
+                                                        ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]),
     "rtKernelSetHitBuffers": (ctypes.c_int, [_vp, _vp, _vp]),
     "rtKernelSetStats": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtKernelSetTiming": (ctypes.c_int, [_vp, ctypes.c_int]),

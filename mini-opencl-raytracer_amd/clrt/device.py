@@ -47,6 +47,18 @@ class CLContext:
         check(self._lib.rtEnqueueCopyBufferToPointer(self.handle, buffer.handle, int(offset), int(size),
                                                      ctypes.c_void_p(int(dst))), "Failed to copy buffer")
 
+    def CopyRectToDevicePointer(self, buffer: "Buffer", src_offset: int, src_pitch: int, width: int,
+                                rows: int, dst: int, dst_pitch: int) -> None:
+        check(self._lib.rtEnqueueCopyBufferRectToPointer(self.handle, buffer.handle, int(src_offset), int(src_pitch),
+                                                         int(width), int(rows), ctypes.c_void_p(int(dst)),
+                                                         int(dst_pitch)), "Failed to copy rect")
+
+    def CopyRectFromDevicePointer(self, src: int, src_pitch: int, buffer: "Buffer", dst_offset: int,
+                                  dst_pitch: int, width: int, rows: int) -> None:
+        check(self._lib.rtEnqueueCopyPointerRectToBuffer(self.handle, ctypes.c_void_p(int(src)), int(src_pitch),
+                                                         buffer.handle, int(dst_offset), int(dst_pitch), int(width),
+                                                         int(rows)), "Failed to copy rect")
+
     def ExecuteKernel(self, kernel: "CLKernel", work_size: int) -> None:
         """enqueueNDRangeKernel(kernel, NullRange, NDRange(workSize)) (CLutils.cpp:44-50)."""
         check(self._lib.rtEnqueueKernel(self.handle, kernel.handle, int(work_size)),
@@ -139,6 +151,9 @@ class CLKernel:
 
     def set_schedule(self, sched: int) -> None:
         check(self._lib.rtKernelSetSchedule(self.handle, int(sched)), "schedule")
+
+    def set_row_interleave(self, period: int, phase: int) -> None:
+        check(self._lib.rtKernelSetRowInterleave(self.handle, int(period), int(phase)), "row interleave")
 
     def set_work_range(self, first: int, last: int) -> None:
         check(self._lib.rtKernelSetWorkRange(self.handle, int(first), int(last)), "work range")

@@ -71,6 +71,7 @@ struct rt_kernel_s {
     int math = RT_MATH_PINNED;
     int sched = RT_SCHED_STEP;
     uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
+    uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
@@ -422,8 +423,15 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.rowBegin = (uint32_t)row0;
     a.rowCount = (uint32_t)(row1 - row0);
     const uint32_t tile = k->sched == RT_SCHED_TILES ? 16u : 8u;
+    if (k->band_period > 1 && k->sched == RT_SCHED_TILES) return RT_INVALID_OPERATION;
     a.tilesX = (W + tile - 1) / tile;
-    const uint64_t tilesY = (row1 - row0 + tile - 1) / tile;
+    uint64_t tilesY = (row1 - row0 + tile - 1) / tile;
+    a.bandPeriod = k->band_period;
+    a.bandPhase = k->band_phase;
+    if (k->band_period > 1) {  // bands phase, phase + period, ... of the row window
+        tilesY = tilesY > k->band_phase ? (tilesY - k->band_phase + k->band_period - 1) / k->band_period : 0;
+        if (tilesY == 0) return RT_SUCCESS;
+    }
     const uint64_t n_tiles = tilesY * a.tilesX;
     if (n_tiles * 64 > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
@@ -529,6 +537,38 @@ int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP) return RT_INVALID_VALUE;
     k->sched = sched;
     return RT_SUCCESS;
+}
+
+int rtKernelSetRowInterleave(rt_kernel k, unsigned period, unsigned phase) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (period == 0 || phase >= period) return RT_INVALID_VALUE;
+    k->band_period = period;
+    k->band_phase = phase;
+    return RT_SUCCESS;
+}
+
+int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offset, size_t src_pitch,
+                                     size_t width_bytes, size_t rows, void* dst, size_t dst_pitch) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!src || src->ctx != ctx || !dst) return RT_INVALID_MEM_OBJECT;
+    if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
+    if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
+    if (src_offset + (rows - 1) * src_pitch + width_bytes > src->size) return RT_INVALID_VALUE;
+    return map_hip(hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
+                                    width_bytes, rows, hipMemcpyDeviceToDevice, ctx->stream));
+}
+
+int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src_pitch, rt_mem dst,
+                                     size_t dst_offset, size_t dst_pitch, size_t width_bytes, size_t rows) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!dst || dst->ctx != ctx || !src) return RT_INVALID_MEM_OBJECT;
+    if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
+    if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
+    if (dst_offset + (rows - 1) * dst_pitch + width_bytes > dst->size) return RT_INVALID_VALUE;
+    return map_hip(hipMemcpy2DAsync(static_cast<uint8_t*>(dst->dptr) + dst_offset, dst_pitch, src, src_pitch,
+                                    width_bytes, rows, hipMemcpyDeviceToDevice, ctx->stream));
 }
 
 int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {

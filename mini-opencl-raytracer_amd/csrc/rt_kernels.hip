@@ -492,7 +492,8 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
                 const uint32_t idx = chunk_base + chunk_used + rank;
                 const uint32_t tile = idx >> 6, w = idx & 63u;
                 const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                const uint32_t x = tx * 8u + (w & 7u), row = a.rowBegin + ty * 8u + (w >> 3);
+                const uint32_t x = tx * 8u + (w & 7u),
+                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
                 const uint64_t g64 = (uint64_t)row * a.width + x;
                 if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                     gid = (uint32_t)g64;
@@ -640,7 +641,8 @@ __global__ __launch_bounds__(256) RT_STEP_OCC void kernel_entry_step(KernelArgs 
                     const uint32_t idx = chunk_base + chunk_used + rank;
                     const uint32_t tile = idx >> 6, w = idx & 63u;
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                    const uint32_t x = tx * 8u + (w & 7u), row = a.rowBegin + ty * 8u + (w >> 3);
+                    const uint32_t x = tx * 8u + (w & 7u),
+                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
                     const uint64_t g64 = (uint64_t)row * a.width + x;
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;

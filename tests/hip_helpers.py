@@ -37,7 +37,7 @@ class HipRenderer:
             self.k.set_hit_buffers(*self.hit_bufs)
 
     def frame(self, frame_count, light_bounces=9, light_type=0, skybox=1.0, camera=DEFAULT_CAMERA,
-              work_range=None):
+              work_range=None, interleave=None):
         k = self.k
         k.set_uint(N.FRAME_COUNT, frame_count)
         k.set_uint(N.FRAME_SEED, 12345)
@@ -49,6 +49,8 @@ class HipRenderer:
         k.set_float3(N.CAMERA_UP, camera[2])
         if work_range is not None:
             k.set_work_range(*work_range)
+        if interleave is not None:
+            k.set_row_interleave(*interleave)
         self.ctx.ExecuteKernel(k, self.n)
 
     def result(self):

@@ -1,0 +1,89 @@
+"""CPU: the multi-GPU sharding path with torch.distributed over gloo (world size 2 and 3).
+
+Each rank renders only its interleaved 8-row bands (here with the CPU oracle standing in
+for the GPU, band by band through its work-item ranges), packs them with the same plan the
+GPU path uses, and the staging buffers are gathered to rank 0 over a real process group;
+the root unpacks them into one image, which must be byte-identical to a single-process
+render of the whole frame.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+W, H, LB = 37, 45, 4  # odd sizes: a short last band and uneven band counts per rank
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    for p in (os.path.join(REPO, "mini-opencl-raytracer_amd"), os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import clrt
+    import oracle
+    from clrt import multigpu as mg
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene = clrt.scene.cornell()
+    img = np.zeros((W * H, 4), np.float32)
+    for f in (1, 2):  # two accumulated frames, as RenderFrame does
+        for b in mg.rank_bands(H, world, rank):
+            r0, r1 = b * mg.BAND_ROWS, min(H, (b + 1) * mg.BAND_ROWS)
+            img, _, _, _ = oracle.render(scene, W, H, frame_count=f, light_bounces=LB, result=img,
+                                         first=r0 * W, last=r1 * W, threads=2)
+    staging = np.zeros(mg.staging_bytes(W, H, world) // 4, np.float32)
+    mg.pack_numpy(img, mg.pack_plan(W, H, world, rank), staging)
+    parts = mg.gather_to_root(dist, torch.from_numpy(staging), rank, world)
+    if rank == 0:
+        full = np.zeros((W * H, 4), np.float32)
+        for r, t in enumerate(parts):
+            mg.unpack_numpy(t.numpy(), mg.pack_plan(W, H, world, r), full)
+        np.save(out_path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_sharded_gather_equals_single_render(tmp_path, cornell, oracle_mod, world):
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    got = np.load(out)
+    want = np.zeros((W * H, 4), np.float32)
+    for f in (1, 2):
+        want, _, _, _ = oracle_mod.render(cornell, W, H, frame_count=f, light_bounces=LB, result=want, threads=2)
+    assert got.tobytes() == want.tobytes()
+
+
+def test_pack_plans_cover_every_row_once():
+    sys.path.insert(0, os.path.join(REPO, "mini-opencl-raytracer_amd"))
+    from clrt import multigpu as mg
+    for (w, h, n) in [(3840, 2160, 8), (1920, 1080, 3), (37, 45, 2), (5, 7, 4), (16, 64, 8)]:
+        hit = np.zeros(h, np.int32)
+        row_bytes = w * mg.PIXEL_BYTES
+        for rank in range(n):
+            used = 0
+            for r in mg.pack_plan(w, h, n, rank):
+                for i in range(r.rows):
+                    start = (r.img_offset + i * r.img_pitch) // row_bytes
+                    nrows = r.width // row_bytes
+                    hit[start:start + nrows] += 1
+                used = max(used, r.stage_offset + r.rows * r.width)
+            assert used <= mg.staging_bytes(w, h, n)
+        assert (hit == 1).all(), (w, h, n)
