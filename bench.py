@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--sched", choices=["regen", "tiles", "step"], default="step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="gloo = dry run of the N>1 flow (host-staged gather; ranks may share a GPU)")
     return p.parse_args()
 
 
@@ -138,15 +140,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist_mod
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            device = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(device)
+            dist_mod.init_process_group("gloo")
         dist = dist_mod
 
     scene = clrt.scene.cornell()
-    r = Rank(scene, args, local, rank, world)
+    r = Rank(scene, args, device, rank, world)
 
     # instrumented pass: ray / node / triangle / hit counts of one step on this rank
     st = count_pass(r)
@@ -155,22 +163,26 @@ def main():
     gather = None
     if dist is not None:
         import torch
-        stage = torch.empty(mg.staging_bytes(r.W, r.H, world) // 4, dtype=torch.float32, device=f"cuda:{local}")
+        stage = torch.empty(mg.staging_bytes(r.W, r.H, world) // 4, dtype=torch.float32, device=f"cuda:{device}")
         plans = [mg.pack_plan(r.W, r.H, world, q) for q in range(world)]
+        host_staged = args.dist_backend == "gloo"
 
         def gather():
             # pack this rank's bands (2-D device copy on the kernel's stream), gather the
             # staging buffers to rank 0 over RCCL, unpack them into rank 0's image
             mg.pack_device(r.ctx, r.out, plans[rank], stage.data_ptr())
             r.finish()
-            parts = mg.gather_to_root(dist, stage, rank, world)
+            parts = mg.gather_to_root(dist, stage.cpu() if host_staged else stage, rank, world)
             if rank == 0:
+                if host_staged:
+                    parts = [p.to(stage.device) for p in parts]
                 torch.cuda.current_stream().synchronize()
                 for q in range(1, world):
                     mg.unpack_device(r.ctx, parts[q].data_ptr(), plans[q], r.out)
                 r.finish()
 
-        tot = torch.tensor(counts, dtype=torch.float64, device=f"cuda:{local}")
+        small_dev = f"cuda:{device}" if args.dist_backend == "nccl" else "cpu"
+        tot = torch.tensor(counts, dtype=torch.float64, device=small_dev)
         dist.all_reduce(tot)
         counts = tot.cpu().numpy()
 
@@ -202,7 +214,7 @@ def main():
     r.k.set_timing(False)
     if dist is not None:
         import torch
-        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
