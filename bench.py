@@ -50,7 +50,9 @@ def parse():
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--bounces", type=int, default=9)
-    p.add_argument("--math", choices=["pinned", "devicelib"], default="pinned")
+    p.add_argument("--math", choices=["pinned", "devicelib"], default="devicelib")
+    p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
+                   help="bunny = the deterministic ~70k-triangle proxy (config 5)")
     p.add_argument("--sched", choices=["regen", "tiles", "step"], default="step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -153,7 +155,11 @@ def main():
             dist_mod.init_process_group("gloo")
         dist = dist_mod
 
-    scene = clrt.scene.cornell()
+    if args.scene == "bunny":
+        import clrt.proxy
+        scene = clrt.proxy.bunny_proxy()
+    else:
+        scene = clrt.scene.cornell()
     r = Rank(scene, args, device, rank, world)
 
     # instrumented pass: ray / node / triangle / hit counts of one step on this rank
@@ -234,7 +240,7 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            key = f"{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
+            key = f"{args.scene}_{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except (ValueError, KeyError):
@@ -244,8 +250,9 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    scene_name = "Cornell box" if args.scene == "cornell" else "bunny-class proxy, 69,692 triangles"
     line = {
-        "metric": "Mrays/s (3840x2160 Cornell box, 8 spp, 9 bounces)",
+        "metric": f"Mrays/s ({args.width}x{args.height} {scene_name}, {args.frames} spp, {args.bounces} bounces)",
         "value": round(value, 3),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -257,8 +264,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "reference scene cornell.obj (scenes/cornell_scene.npz); rays generated in-kernel",
-        "config": {"workload": f"cornell {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
+        "data": ("reference scene cornell.obj (scenes/cornell_scene.npz)" if args.scene == "cornell" else
+                 "generated bunny-class proxy OBJ (clrt/proxy.py)") + "; rays generated in-kernel",
+        "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
                    "math": args.math, "schedule": args.sched, "parallelism": f"interleaved 8-row bands x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},

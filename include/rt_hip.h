@@ -100,8 +100,8 @@ int rtFinish(rt_context ctx);
 int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset, size_t size,
                          const void* src);
 
-/* Math policy of the kernel: RT_MATH_PINNED (default; bit-identical to the pinned CPU
- * semantics of rt_pinned_math.h) or RT_MATH_DEVICELIB (the AMD OpenCL device-library
+/* Math policy of the kernel: RT_MATH_PINNED (bit-identical to the pinned CPU
+ * semantics of rt_pinned_math.h) or RT_MATH_DEVICELIB (default: the AMD OpenCL device-library
  * builtins the reference kernel gets on this GPU). */
 #define RT_MATH_PINNED 0
 #define RT_MATH_DEVICELIB 1

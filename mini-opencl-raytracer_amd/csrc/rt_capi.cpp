@@ -68,7 +68,7 @@ struct rt_kernel_s {
     rt_mem bufs[4] = {};
     uint32_t u32[RT_ARG_COUNT] = {};  // slots 4..10 (raw 4-byte values)
     float f3[3][4] = {};              // slots 11..13
-    int math = RT_MATH_PINNED;
+    int math = RT_MATH_DEVICELIB;
     int sched = RT_SCHED_STEP;
     uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)

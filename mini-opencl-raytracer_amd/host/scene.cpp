@@ -286,7 +286,7 @@ rt_cl_vertex make_vertex(const V3& p, float u, float v, const V3& n) {
 // CLOBJloader::LoadTriangles (CLOBJloader.cpp:16-129)
 int load_obj(const char* path, rt_scene* s) {
     const size_t len = std::strlen(path);
-    if (len < 4 || len >= 80) return RT_INVALID_VALUE;
+    if (len < 4) return RT_INVALID_VALUE;  // (the reference copies into char[80]; no such limit here)
     std::string mtl(path, len - 4);
     mtl += ".mtl";
     int rc = load_mtl(mtl.c_str(), s);
