@@ -156,8 +156,8 @@ def main():
         dist = dist_mod
 
     if args.scene == "bunny":
-        import clrt.proxy
-        scene = clrt.proxy.bunny_proxy()
+        from clrt import proxy as clrt_proxy
+        scene = clrt_proxy.bunny_proxy()
     else:
         scene = clrt.scene.cornell()
     r = Rank(scene, args, device, rank, world)

@@ -16,3 +16,4 @@ step sq1 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WA
 step sq2 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/p_sq2 -o run -- $B
 step sq3 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_VALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/p_sq3 -o run -- $B
 python scripts/pmc_summary.py $OUT/summary.json $OUT/p_fetch $OUT/p_write $OUT/p_sq1 $OUT/p_sq2 $OUT/p_sq3
+cp $OUT/trace/run_kernel_stats.csv $OUT/kernel_stats.csv 2>/dev/null || true
