@@ -39,8 +39,14 @@
 
 #if defined(__HIPCC__)
 #define RT_PM_FN __host__ __device__ static inline
+/* the fp64 transcendentals stay out of line in device code: six inlined pow expansions in
+ * the pixel-accumulation step would otherwise overlap and cost the kernel ~30 VGPRs */
+#ifndef RT_PM_HEAVY
+#define RT_PM_HEAVY __attribute__((noinline)) __host__ __device__ static
+#endif
 #else
 #define RT_PM_FN static inline
+#define RT_PM_HEAVY static inline
 #endif
 
 #if defined(__HIPCC__) || defined(__clang__)
@@ -257,7 +263,7 @@ RT_PM_FN int pm_is_odd_int(float y) {
 }
 
 /* OpenCL/C99 pow special cases, then 2^(y*log2|x|) in fp64, rounded once */
-RT_PM_FN float pm_pow(float x, float y) {
+RT_PM_HEAVY float pm_pow(float x, float y) {
     const float qnan = pm_u2f(0x7fc00000u);
     if (y == 0.0f) return 1.0f;
     if (x == 1.0f) return 1.0f;

@@ -71,6 +71,7 @@ struct rt_kernel_s {
     int math = RT_MATH_DEVICELIB;
     int sched = RT_SCHED_STEP;
     uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
+    uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
@@ -325,6 +326,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     k->ctx = ctx;
     if (const char* v = std::getenv("RT_REFILL_MIN")) k->refill_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
+    if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
@@ -438,6 +441,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.workCounter = k->work_counter;
     a.refillMin = k->refill_min;
     a.shadeMin = k->shade_min;
+    a.stepWeightNode = k->w_node;
+    a.stepWeightLeaf = k->w_leaf;
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;

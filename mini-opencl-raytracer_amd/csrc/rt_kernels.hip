@@ -554,14 +554,8 @@ constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
-#ifdef RT_STEP_WAVES_PER_EU
-#define RT_STEP_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_WAVES_PER_EU, 8)))
-#else
-#define RT_STEP_OCC
-#endif
-
 template <class M, bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) RT_STEP_OCC void kernel_entry_step(KernelArgs a) {
+__device__ __forceinline__ void step_body(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
     const float4* nodes;
@@ -678,40 +672,50 @@ __global__ __launch_bounds__(256) RT_STEP_OCC void kernel_entry_step(KernelArgs 
         }
 
         // ---- traversal steps -----------------------------------------------------------------
+        // Each step is wave-uniform: either a node step (TRAV lanes visit one node) or a
+        // triangle step (LEAF lanes test one triangle), chosen by which serves more lanes per
+        // instruction (weights ~ the two bodies' VALU cost), so the wave never pays both
+        // bodies for a mix of lanes.
         for (;;) {
-            const unsigned long long busy = __ballot(state == kTrav || state == kLeaf);
-            if (busy == 0ull) break;
+            const uint32_t n_trav = popc_ballot(state == kTrav);
+            const uint32_t n_leaf = popc_ballot(state == kLeaf);
+            if (n_trav + n_leaf == 0u) break;
             if (popc_ballot(state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
+            const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
             bool pop = false;
-            if (state == kTrav) {
-                const float4 q0 = nodes[2 * cur];
-                const float4 q1 = nodes[2 * cur + 1];
-                if (kStats) ++st.visits;
-                pop = true;
-                if (ray_bounds(q0, q1, ray, h.t)) {
-                    const uint32_t off = __float_as_uint(q1.z);
-                    const uint32_t meta = __float_as_uint(q1.w);
-                    const uint32_t np = meta & 0xffffu;
-                    if (np > 0) {
-                        state = kLeaf;
-                        leaf_i = off;
-                        leaf_end = off + np;
-                        pop = false;
-                    } else {
-                        const uint32_t axis = meta >> 16;
-                        const bool far_first = (ray.sgn >> axis) & 1u;
-                        stack[sp * 256] = far_first ? cur + 1 : (int)off;
-                        ++sp;
-                        cur = far_first ? (int)off : cur + 1;
-                        pop = false;
+            if (!leaf_step) {
+                if (state == kTrav) {
+                    const float4 q0 = nodes[2 * cur];
+                    const float4 q1 = nodes[2 * cur + 1];
+                    if (kStats) ++st.visits;
+                    pop = true;
+                    if (ray_bounds(q0, q1, ray, h.t)) {
+                        const uint32_t off = __float_as_uint(q1.z);
+                        const uint32_t meta = __float_as_uint(q1.w);
+                        const uint32_t np = meta & 0xffffu;
+                        if (np > 0) {
+                            state = kLeaf;
+                            leaf_i = off;
+                            leaf_end = off + np;
+                            pop = false;
+                        } else {
+                            const uint32_t axis = meta >> 16;
+                            const bool far_first = (ray.sgn >> axis) & 1u;
+                            stack[sp * 256] = far_first ? cur + 1 : (int)off;
+                            ++sp;
+                            cur = far_first ? (int)off : cur + 1;
+                            pop = false;
+                        }
                     }
                 }
-            } else if (state == kLeaf) {
-                if (kStats) ++st.tests;
-                ray_triangle<M>(tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                ++leaf_i;
-                pop = leaf_i == leaf_end;
+            } else {
+                if (state == kLeaf) {
+                    if (kStats) ++st.tests;
+                    ray_triangle<M>(tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                    ++leaf_i;
+                    pop = leaf_i == leaf_end;
+                }
             }
             if (pop) {
                 if (sp == 0) {
@@ -758,6 +762,27 @@ __global__ __launch_bounds__(256) RT_STEP_OCC void kernel_entry_step(KernelArgs 
     }
 }
 
+// Entry points per math policy: the devicelib body fits 80 VGPRs with a small spill, and
+// 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
+// (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
+#ifndef RT_STEP_DEVICELIB_WAVES
+#define RT_STEP_DEVICELIB_WAVES 6
+#endif
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
+void kernel_entry_step_devicelib(KernelArgs a) {
+    step_body<MathDeviceLib, kLdsScene, kStats>(a);
+}
+#ifdef RT_STEP_PINNED_WAVES
+#define RT_STEP_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
+#else
+#define RT_STEP_PINNED_OCC
+#endif
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
+    step_body<MathPinned, kLdsScene, kStats>(a);
+}
+
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
 __global__ void pack_nodes(const rt_cl_bvh_node* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -789,7 +814,10 @@ using KernelFn = void (*)(KernelArgs);
 
 template <class M, bool L, bool S>
 static KernelFn pick_sched(int sched) {
-    if (sched == kSchedStep) return kernel_entry_step<M, L, S>;
+    if (sched == kSchedStep) {
+        if (M::kId == MathDeviceLib::kId) return kernel_entry_step_devicelib<L, S>;
+        return kernel_entry_step_pinned<L, S>;
+    }
     return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
 }
 

@@ -27,6 +27,7 @@ struct KernelArgs {
     uint32_t rowBegin, rowCount, tilesX, nTiles;  // tiles: 16x16 (tile schedule) or 8x8 (regen)
     uint32_t* workCounter;              // regen schedule: next 64-pixel chunk (zeroed per launch)
     uint32_t refillMin, shadeMin;       // step schedule batching thresholds (lanes)
+    uint32_t stepWeightNode, stepWeightLeaf;  // step schedule: relative cost of node / triangle steps
     uint32_t bandPeriod, bandPhase;     // 8-row bands: this launch renders bands b % period == phase
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
