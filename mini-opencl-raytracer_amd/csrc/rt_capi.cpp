@@ -30,7 +30,6 @@ namespace {
 constexpr uint64_t kKnownFlags =
     RT_MEM_READ_WRITE | RT_MEM_WRITE_ONLY | RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
 constexpr int kStatWords = 8;                 // rt_stats counters kept on the device
-constexpr int kMaxStack = 64;                  // nodesToVisit[64], kernel_bvh.cl:181
 constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
 
 int map_hip(hipError_t e) {
@@ -87,7 +86,8 @@ struct rt_kernel_s {
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
     float4* packed_nodes = nullptr;
     float4* packed_tris = nullptr;
-    size_t packed_nodes_cap = 0, packed_tris_cap = 0;
+    uint32_t* packed_skips = nullptr;
+    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
@@ -138,7 +138,28 @@ int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* dept
         }
     }
     *depth_out = max_depth;
-    return max_depth > kMaxStack ? RT_INVALID_MEM_OBJECT : RT_SUCCESS;
+    // The reference's 64-entry stack (kernel_bvh.cl:181) would overflow past depth 64; the
+    // stackless walk here has no such limit, so deeper trees are rendered, not rejected.
+    return RT_SUCCESS;
+}
+
+// Per-octant skip pointers (see rt_kernels.hip, intersect): for octant o (bit i = the ray
+// direction's sign on axis i) the reference visits an interior node's second child first
+// when bit axis(n) is set (kernel_bvh.cl:200-207).  skip[n][o] is the node the reference
+// pops after finishing n's subtree: near child -> far child, far child -> skip of parent.
+// Children have larger indices than their parent, so one forward sweep fills the table.
+void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& skips) {
+    skips.assign((size_t)n * 8, 0xffffffffu);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (nd[i].nPrimitives > 0) continue;
+        const uint32_t first = i + 1, second = nd[i].offset;
+        for (uint32_t o = 0; o < 8; ++o) {
+            const bool swap = (o >> nd[i].axis) & 1u;
+            const uint32_t nearc = swap ? second : first, farc = swap ? first : second;
+            skips[(size_t)nearc * 8 + o] = farc;
+            skips[(size_t)farc * 8 + o] = skips[(size_t)i * 8 + o];
+        }
+    }
 }
 
 int prepare_scene(rt_kernel k) {
@@ -167,6 +188,8 @@ int prepare_scene(rt_kernel k) {
     const rt_cl_triangle* tr = reinterpret_cast<const rt_cl_triangle*>(tb);
     for (uint32_t i = 0; i < nt; ++i)
         if (tr[i].mtlIndex >= nmat) return RT_INVALID_MEM_OBJECT;
+    std::vector<uint32_t> skips;
+    build_skips(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips);
 
     if (k->packed_nodes_cap < (size_t)nn) {
         if (k->packed_nodes) (void)hipFree(k->packed_nodes);
@@ -175,6 +198,20 @@ int prepare_scene(rt_kernel k) {
         hipError_t e = hipMalloc(&k->packed_nodes, (size_t)nn * 2 * sizeof(float4));
         if (e != hipSuccess) return map_hip(e);
         k->packed_nodes_cap = nn;
+    }
+    if (k->packed_skips_cap < (size_t)nn) {
+        if (k->packed_skips) (void)hipFree(k->packed_skips);
+        k->packed_skips = nullptr;
+        k->packed_skips_cap = 0;
+        hipError_t e = hipMalloc(&k->packed_skips, (size_t)nn * 8 * sizeof(uint32_t));
+        if (e != hipSuccess) return map_hip(e);
+        k->packed_skips_cap = nn;
+    }
+    {
+        hipError_t e = hipMemcpyAsync(k->packed_skips, skips.data(), skips.size() * sizeof(uint32_t),
+                                      hipMemcpyHostToDevice, k->ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+        if (e != hipSuccess) return map_hip(e);
     }
     if (k->packed_tris_cap < (size_t)nt) {
         if (k->packed_tris) (void)hipFree(k->packed_tris);
@@ -352,6 +389,7 @@ int rtReleaseKernel(rt_kernel k) {
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
     if (k->packed_nodes) (void)hipFree(k->packed_nodes);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
+    if (k->packed_skips) (void)hipFree(k->packed_skips);
     if (k->dstats) (void)hipFree(k->dstats);
     if (k->work_counter) (void)hipFree(k->work_counter);
     delete k;
@@ -407,6 +445,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.materials = static_cast<const rt_cl_material*>(k->bufs[RT_ARG_BUFFER_MATERIAL]->dptr);
     a.packedNodes = k->packed_nodes;
     a.packedTris = k->packed_tris;
+    a.skips = k->packed_skips;
     a.nNodes = k->n_nodes;
     a.nTris = k->n_tris;
     a.width = W;
@@ -447,11 +486,10 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
 
-    const size_t stack_bytes = (size_t)std::max(1, k->depth) * 256 * sizeof(int);
-    const size_t scene_bytes = (size_t)k->n_nodes * 32 + (size_t)k->n_tris * 48;
-    const bool lds = !k->force_global && scene_bytes + stack_bytes <= kLdsBudget;
-    const size_t smem = lds ? scene_bytes + stack_bytes : stack_bytes;
-    if (smem > kLdsBudget) return RT_OUT_OF_RESOURCES;
+    // LDS: packed nodes (32 B) + triangles (48 B) + skip pointers (32 B per node); no stack
+    const size_t scene_bytes = (size_t)k->n_nodes * 64 + (size_t)k->n_tris * 48;
+    const bool lds = !k->force_global && scene_bytes <= kLdsBudget;
+    const size_t smem = lds ? scene_bytes : 0;
     k->last_lds = lds;
 
     const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;

@@ -11,9 +11,11 @@
 //     and triangles into 48-byte {p1, e1 = p2-p1, e2 = p3-p1} records (three b128
 //     reads); both live in LDS when they fit (Cornell: 4.7 KB), else they are read from
 //     HBM/L2 through the same code (global path);
-//   * the traversal stack is per lane in LDS, laid out [depth][lane] so the 64 lanes of
-//     a wave hit 64 different banks; its depth is the tree depth (host-computed), not
-//     the reference's fixed 64;
+//   * no traversal stack: the reference's stack walk (push the far child, pop on a miss
+//     or after a leaf) is a depth-first order whose child order depends only on the
+//     ray's octant, so it is replayed exactly with per-octant skip pointers (8 per
+//     node, built on the host): node visits, triangle tests and their order are the
+//     reference's, without LDS pushes/pops or the dependent pop latency;
 //   * traversal keeps only {t, primitive, u, v}; the hit record (position, shading
 //     normal, material) is formed once after the walk from the last accepted triangle,
 //     which yields the same values as the reference forming it at every accept;
@@ -90,9 +92,31 @@ __device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, 
 // Packed node: q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y, bmax.z, offset, meta),
 // meta = nPrimitives | axis << 16.  Packed triangle: p1, e1, e2 (w unused).
 struct SceneView {
-    const float4* nodes;  // LDS or global
-    const float4* tris;   // LDS or global
+    const float4* nodes;    // LDS or global
+    const float4* tris;     // LDS or global
+    const uint32_t* skips;  // [node][octant]: next node in this octant's DFS order after the subtree
 };
+
+constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
+
+// Scene into LDS once per workgroup (when it fits), else read in place.
+template <bool kLdsScene>
+__device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    if (kLdsScene) {
+        const int tid = threadIdx.x;
+        float4* ln = smem;
+        float4* lt = smem + 2 * a.nNodes;
+        float4* lk = lt + 3 * a.nTris;
+        const float4* gk = reinterpret_cast<const float4*>(a.skips);
+        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
+        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) lk[i] = gk[i];
+        __syncthreads();
+        return SceneView{ln, lt, reinterpret_cast<const uint32_t*>(lk)};
+    }
+    return SceneView{a.packedNodes, a.packedTris, a.skips};
+}
 
 struct Traversal {
     float t;
@@ -143,19 +167,20 @@ __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, con
     }
 }
 
-// kernel_bvh.cl:171-219 (Intersect).  `stack` points at this lane's column of the
-// workgroup's LDS stack ([depth][256]).
+// kernel_bvh.cl:171-219 (Intersect), replayed with the per-octant skip pointers: visiting
+// a node whose box is missed -- or finishing a leaf -- continues at skip[node][octant], the
+// node the reference pops next; a passed interior node continues at its near child
+// (the second child when sign[axis], kernel_bvh.cl:200-207).
 template <class M, bool kStats>
-__device__ __forceinline__ Traversal intersect(const SceneView& sc, const Ray& r, int* stack,
-                                               uint32_t& visits, uint32_t& tests) {
+__device__ __forceinline__ Traversal intersect(const SceneView& sc, const Ray& r, uint32_t& visits,
+                                               uint32_t& tests) {
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    int sp = 0;
-    int cur = 0;
-    for (;;) {
+    uint32_t cur = 0;
+    while (cur != kEnd) {
         const float4 q0 = sc.nodes[2 * cur];
         const float4 q1 = sc.nodes[2 * cur + 1];
+        const uint32_t skip = sc.skips[8 * cur + r.sgn];
         if (kStats) ++visits;
-        bool pop = true;
         if (ray_bounds(q0, q1, r, h.t)) {
             const uint32_t off = __float_as_uint(q1.z);
             const uint32_t meta = __float_as_uint(q1.w);
@@ -165,19 +190,12 @@ __device__ __forceinline__ Traversal intersect(const SceneView& sc, const Ray& r
                     if (kStats) ++tests;
                     ray_triangle<M>(sc.tris + 3 * (size_t)(off + i), (int32_t)(off + i), r, h);
                 }
+                cur = skip;
             } else {
-                const uint32_t axis = meta >> 16;
-                const bool far_first = (r.sgn >> axis) & 1u;
-                stack[sp * 256] = far_first ? cur + 1 : (int)off;
-                ++sp;
-                cur = far_first ? (int)off : cur + 1;
-                pop = false;
+                cur = ((r.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
             }
-        }
-        if (pop) {
-            if (sp == 0) break;
-            --sp;
-            cur = stack[sp * 256];
+        } else {
+            cur = skip;
         }
     }
     return h;
@@ -309,13 +327,13 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
 template <class M, bool kStats>
 __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* __restrict__ tris_full,
                                      const rt_cl_material* __restrict__ mats, Ray ray,
-                                     uint32_t& seed, const KernelArgs& a, int* stack,
+                                     uint32_t& seed, const KernelArgs& a,
                                      int32_t& prim_id, float& prim_t, LaneStats& st) {
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     const uint32_t bounces = (uint32_t)a.lightBounces;
     for (uint32_t i = 0; i < bounces; ++i) {
         if (kStats) ++st.rays;
-        const Traversal h = intersect<M, kStats>(sc, ray, stack, st.visits, st.tests);
+        const Traversal h = intersect<M, kStats>(sc, ray, st.visits, st.tests);
         if (i == 0) {
             prim_id = h.prim;
             prim_t = h.t;
@@ -366,27 +384,8 @@ __device__ __forceinline__ void flush_stats(const KernelArgs& a, const LaneStats
 // ---- the kernel (tile schedule) ------------------------------------------------------------
 template <class M, bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
-    const float4* nodes;
-    const float4* tris;
-    int* stack_base;
-    if (kLdsScene) {
-        float4* ln = smem;
-        float4* lt = smem + 2 * a.nNodes;
-        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
-        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-        nodes = ln;
-        tris = lt;
-        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
-        __syncthreads();
-    } else {
-        nodes = a.packedNodes;
-        tris = a.packedTris;
-        stack_base = reinterpret_cast<int*>(smem);
-    }
-    int* stack = stack_base + tid;
-    const SceneView sc{nodes, tris};
+    const SceneView sc = stage_scene<kLdsScene>(a);
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
@@ -412,7 +411,7 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
         const Ray ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
         int32_t pid = -1;
         float pt = 0.0f;
-        const F3 rad = render<M, kStats>(sc, a.trisFull, a.materials, ray, seed, a, stack, pid, pt, st);
+        const F3 rad = render<M, kStats>(sc, a.trisFull, a.materials, ray, seed, a, pid, pt, st);
         finish_pixel<M>(a, gid, rad, pid, pt);
     }
     if (kStats) flush_stats(a, st, lane);
@@ -427,27 +426,8 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
 // reference's exact sequence of operations with its own seed, so results are identical.
 template <class M, bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
-    const float4* nodes;
-    const float4* tris;
-    int* stack_base;
-    if (kLdsScene) {
-        float4* ln = smem;
-        float4* lt = smem + 2 * a.nNodes;
-        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
-        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-        nodes = ln;
-        tris = lt;
-        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
-        __syncthreads();
-    } else {
-        nodes = a.packedNodes;
-        tris = a.packedTris;
-        stack_base = reinterpret_cast<int*>(smem);
-    }
-    int* stack = stack_base + tid;
-    const SceneView sc{nodes, tris};
+    const SceneView sc = stage_scene<kLdsScene>(a);
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
@@ -520,7 +500,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
         // ---- one bounce of every live path -------------------------------------------------
         if (active) {
             if (kStats) ++st.rays;
-            const Traversal h = intersect<M, kStats>(sc, ray, stack, st.visits, st.tests);
+            const Traversal h = intersect<M, kStats>(sc, ray, st.visits, st.tests);
             if (bounce == 0u) {
                 pid = h.prim;
                 pt = h.t;
@@ -556,26 +536,8 @@ __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__pop
 
 template <class M, bool kLdsScene, bool kStats>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
-    const float4* nodes;
-    const float4* tris;
-    int* stack_base;
-    if (kLdsScene) {
-        float4* ln = smem;
-        float4* lt = smem + 2 * a.nNodes;
-        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
-        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-        nodes = ln;
-        tris = lt;
-        stack_base = reinterpret_cast<int*>(smem + 2 * a.nNodes + 3 * a.nTris);
-        __syncthreads();
-    } else {
-        nodes = a.packedNodes;
-        tris = a.packedTris;
-        stack_base = reinterpret_cast<int*>(smem);
-    }
-    int* stack = stack_base + tid;
+    const SceneView sc = stage_scene<kLdsScene>(a);
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
@@ -597,7 +559,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     Ray ray{};
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    int sp = 0, cur = 0;
+    uint32_t cur = 0;  // TRAV: node to visit; LEAF: node to continue at after the leaf
     uint32_t leaf_i = 0, leaf_end = 0;
     uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
     bool exhausted = false;                    // wave-uniform
@@ -650,7 +612,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if (bounces > 0u) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                            sp = 0;
                             cur = 0;
                             if (kStats) ++st.rays;
                         } else {
@@ -683,13 +644,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (popc_ballot(state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
-            bool pop = false;
             if (!leaf_step) {
                 if (state == kTrav) {
-                    const float4 q0 = nodes[2 * cur];
-                    const float4 q1 = nodes[2 * cur + 1];
+                    const float4 q0 = sc.nodes[2 * cur];
+                    const float4 q1 = sc.nodes[2 * cur + 1];
+                    const uint32_t skip = sc.skips[8 * cur + ray.sgn];
                     if (kStats) ++st.visits;
-                    pop = true;
+                    uint32_t next = skip;
                     if (ray_bounds(q0, q1, ray, h.t)) {
                         const uint32_t off = __float_as_uint(q1.z);
                         const uint32_t meta = __float_as_uint(q1.w);
@@ -698,32 +659,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             state = kLeaf;
                             leaf_i = off;
                             leaf_end = off + np;
-                            pop = false;
                         } else {
-                            const uint32_t axis = meta >> 16;
-                            const bool far_first = (ray.sgn >> axis) & 1u;
-                            stack[sp * 256] = far_first ? cur + 1 : (int)off;
-                            ++sp;
-                            cur = far_first ? (int)off : cur + 1;
-                            pop = false;
+                            next = ((ray.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
                         }
                     }
+                    cur = next;
+                    if (state == kTrav && next == kEnd) state = kShade;
                 }
             } else {
                 if (state == kLeaf) {
                     if (kStats) ++st.tests;
-                    ray_triangle<M>(tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                    ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
                     ++leaf_i;
-                    pop = leaf_i == leaf_end;
-                }
-            }
-            if (pop) {
-                if (sp == 0) {
-                    state = kShade;
-                } else {
-                    --sp;
-                    cur = stack[sp * 256];
-                    state = kTrav;
+                    if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
                 }
             }
         }
@@ -744,7 +692,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             } else {
                 state = kTrav;
                 h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                sp = 0;
                 cur = 0;
                 if (kStats) ++st.rays;
             }

@@ -16,6 +16,7 @@ struct KernelArgs {
     const rt_cl_material* materials;    // slot 3
     const float4* packedNodes;          // derived from slot 2: 2 x float4 per node
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
+    const uint32_t* skips;              // derived from slot 2: [node][octant] DFS skip pointers
     uint32_t nNodes, nTris;
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)
