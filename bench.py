@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--math", choices=["pinned", "devicelib"], default="devicelib")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
-    p.add_argument("--sched", choices=["regen", "tiles", "step"], default="step")
+    p.add_argument("--sched", choices=["regen", "tiles", "step", "pool"], default="step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -93,7 +93,8 @@ class Rank:
         k.set_float3(N.CAMERA_FRONT, CAMERA[1])
         k.set_float3(N.CAMERA_UP, CAMERA[2])
         k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
-        k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP}[args.sched])
+        k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
+                        "pool": N.SCHED_POOL}[args.sched])
         k.set_row_interleave(world, rank)
 
     def render(self):

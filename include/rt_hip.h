@@ -113,10 +113,14 @@ int rtKernelSetMathMode(rt_kernel k, int mode);
  * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles);
  * RT_SCHED_STEP (default)  -- per-wave state machine: every step advances each lane by one
  *                             BVH node or one triangle; shading and pixel refill run when
- *                             enough lanes are ready. */
+ *                             enough lanes are ready;
+ * RT_SCHED_POOL            -- step traversal, plus a per-wave LDS pool of 64 path records:
+ *                             lanes park finished traversals and keep tracing; shading runs
+ *                             64 records at a time. */
 #define RT_SCHED_TILES 0
 #define RT_SCHED_REGEN 1
 #define RT_SCHED_STEP 2
+#define RT_SCHED_POOL 3
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
 /* Restrict the next launches to work-items [first, last) (pixel-row tiles for
@@ -149,6 +153,11 @@ typedef struct rt_stats {
     /* diagnostic (step schedule, stats on): shader-clock cycles summed over waves spent
      * refilling/finishing pixels, traversing, shading, and in total */
     uint64_t cycles_refill, cycles_traverse, cycles_shade, cycles_total;
+    /* diagnostic (step schedule, stats on): node steps, lanes served by node steps,
+     * triangle steps, lanes served, shading rounds, lanes shaded, refill rounds, lanes freed,
+     * then summed over all steps: lanes of the other traversal kind, lanes waiting to shade,
+     * free lanes, reserved */
+    uint64_t sched[12];
 } rt_stats;
 int rtKernelSetStats(rt_kernel k, int enable);
 int rtKernelSetTiming(rt_kernel k, int enable);

@@ -70,7 +70,7 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB = 0, 1
-SCHED_TILES, SCHED_REGEN, SCHED_STEP = 0, 1, 2
+SCHED_TILES, SCHED_REGEN, SCHED_STEP, SCHED_POOL = 0, 1, 2, 3
 
 
 class Stats(ctypes.Structure):
@@ -78,7 +78,8 @@ class Stats(ctypes.Structure):
                 ("tri_tests", ctypes.c_uint64), ("hits", ctypes.c_uint64),
                 ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("cycles_refill", ctypes.c_uint64), ("cycles_traverse", ctypes.c_uint64),
-                ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64)]
+                ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64),
+                ("sched", ctypes.c_uint64 * 12)]
 
 
 _vp = ctypes.c_void_p

@@ -183,7 +183,10 @@ class CLKernel:
         return {"rays": s.rays, "node_visits": s.node_visits, "tri_tests": s.tri_tests,
                 "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms,
                 "cycles": {"refill": s.cycles_refill, "traverse": s.cycles_traverse,
-                           "shade": s.cycles_shade, "total": s.cycles_total}}
+                           "shade": s.cycles_shade, "total": s.cycles_total},
+                "sched": dict(zip(("node_steps", "node_lanes", "tri_steps", "tri_lanes", "shade_rounds",
+                                   "shade_lanes", "refill_rounds", "refill_lanes", "other_lanes",
+                                   "shade_wait", "free_wait", "reserved"), list(s.sched)))}
 
     def reset_stats(self) -> None:
         check(self._lib.rtKernelResetStats(self.handle), "reset stats")

@@ -29,7 +29,7 @@ namespace {
 
 constexpr uint64_t kKnownFlags =
     RT_MEM_READ_WRITE | RT_MEM_WRITE_ONLY | RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
-constexpr int kStatWords = 8;                 // rt_stats counters kept on the device
+constexpr int kStatWords = 20;                // rt_stats counters kept on the device
 constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
 
 int map_hip(hipError_t e) {
@@ -71,6 +71,7 @@ struct rt_kernel_s {
     int sched = RT_SCHED_STEP;
     uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
+    uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
@@ -87,12 +88,14 @@ struct rt_kernel_s {
     float4* packed_nodes = nullptr;
     float4* packed_tris = nullptr;
     uint32_t* packed_skips = nullptr;
-    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0;
+    float4* oct_nodes = nullptr;       // [node][octant] 2 x float4 (LDS-resident scenes)
+    uint32_t* leaf_ext = nullptr;      // {first, count} of leaves the octant records cannot encode
+    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0, leaf_ext_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[3][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
-    size_t occ_smem[3][2][2][2] = {};
+    int occ_cache[rtk::kNumSched][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
+    size_t occ_smem[rtk::kNumSched][2][2][2] = {};
 };
 
 namespace {
@@ -162,6 +165,70 @@ void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& sk
     }
 }
 
+// Octant-resolved node records for LDS-resident scenes: for node n and ray octant o,
+//   A = {near.x, near.y, near.z, far.x}, B = {far.y, far.z, hit_next, miss_next}
+// where near/far are the slab planes kernel_bvh.cl:156-169 selects by the ray's signs
+// (bit-exact copies of pmin/pmax), miss_next = skip[n][o] and hit_next is the near child
+// (interior) or the leaf {first, count}: bit 31 set, then either count-1 (6 bits) and
+// first (24 bits), or bit 30 + an index into leaf_ext for leaves outside those ranges.
+// A node step is then two b128 reads, the slab arithmetic and one select.
+constexpr uint32_t kLeafBit = 0x80000000u, kLeafExtBit = 0x40000000u;
+
+void build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
+                     std::vector<uint32_t>& out, std::vector<uint32_t>& ext) {
+    out.assign((size_t)n * 8 * 8, 0u);
+    ext.clear();
+    auto bits = [](float f) {
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        return u;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+        const rt_cl_bvh_node& x = nd[i];
+        uint32_t leaf = 0;
+        if (x.nPrimitives > 0) {
+            if (x.offset < (1u << 24) && x.nPrimitives <= 64) {
+                leaf = kLeafBit | ((uint32_t)(x.nPrimitives - 1) << 24) | x.offset;
+            } else {
+                leaf = kLeafBit | kLeafExtBit | (uint32_t)(ext.size() / 2);
+                ext.push_back(x.offset);
+                ext.push_back(x.nPrimitives);
+            }
+        }
+        const float lo[3] = {x.bounds.pmin.x, x.bounds.pmin.y, x.bounds.pmin.z};
+        const float hi[3] = {x.bounds.pmax.x, x.bounds.pmax.y, x.bounds.pmax.z};
+        for (uint32_t o = 0; o < 8; ++o) {
+            uint32_t* r = &out[((size_t)i * 8 + o) * 8];
+            float nr[3], fr[3];
+            for (int ax = 0; ax < 3; ++ax) {
+                const bool neg = (o >> ax) & 1u;
+                nr[ax] = neg ? hi[ax] : lo[ax];
+                fr[ax] = neg ? lo[ax] : hi[ax];
+            }
+            r[0] = bits(nr[0]);
+            r[1] = bits(nr[1]);
+            r[2] = bits(nr[2]);
+            r[3] = bits(fr[0]);
+            r[4] = bits(fr[1]);
+            r[5] = bits(fr[2]);
+            r[6] = x.nPrimitives > 0 ? leaf : (((o >> x.axis) & 1u) ? x.offset : i + 1);
+            r[7] = skips[(size_t)i * 8 + o];
+        }
+    }
+}
+
+template <class T>
+int ensure_dev(T*& p, size_t& cap, size_t count) {
+    if (cap >= count) return RT_SUCCESS;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e != hipSuccess) return map_hip(e);
+    cap = count;
+    return RT_SUCCESS;
+}
+
 int prepare_scene(rt_kernel k) {
     rt_mem tm = k->bufs[RT_ARG_BUFFER_SCENE], nm = k->bufs[RT_ARG_BUFFER_NODE],
            mm = k->bufs[RT_ARG_BUFFER_MATERIAL];
@@ -201,15 +268,29 @@ int prepare_scene(rt_kernel k) {
     }
     if (k->packed_skips_cap < (size_t)nn) {
         if (k->packed_skips) (void)hipFree(k->packed_skips);
+    if (k->oct_nodes) (void)hipFree(k->oct_nodes);
+    if (k->leaf_ext) (void)hipFree(k->leaf_ext);
         k->packed_skips = nullptr;
         k->packed_skips_cap = 0;
         hipError_t e = hipMalloc(&k->packed_skips, (size_t)nn * 8 * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip(e);
         k->packed_skips_cap = nn;
     }
+    std::vector<uint32_t> oct, ext;
+    build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct, ext);
+    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)nn * 16);
+    if (rc) return rc;
+    rc = ensure_dev(k->leaf_ext, k->leaf_ext_cap, std::max<size_t>(2, ext.size()));
+    if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->packed_skips, skips.data(), skips.size() * sizeof(uint32_t),
                                       hipMemcpyHostToDevice, k->ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               k->ctx->stream);
+        if (e == hipSuccess && !ext.empty())
+            e = hipMemcpyAsync(k->leaf_ext, ext.data(), ext.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               k->ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
         if (e != hipSuccess) return map_hip(e);
     }
@@ -365,6 +446,13 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
+    if (const char* v = std::getenv("RT_POOL_SHADE")) k->pool_shade = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_PARK_MIN")) k->park_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_LOW_WORK")) k->low_work = (uint32_t)std::max(1, std::min(128, std::atoi(v)));
+    if (const char* v = std::getenv("RT_SCHED")) {
+        const int sv = std::atoi(v);
+        if (sv >= 0 && sv < rtk::kNumSched) k->sched = sv;
+    }
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
@@ -390,6 +478,8 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->packed_nodes) (void)hipFree(k->packed_nodes);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->packed_skips) (void)hipFree(k->packed_skips);
+    if (k->oct_nodes) (void)hipFree(k->oct_nodes);
+    if (k->leaf_ext) (void)hipFree(k->leaf_ext);
     if (k->dstats) (void)hipFree(k->dstats);
     if (k->work_counter) (void)hipFree(k->work_counter);
     delete k;
@@ -446,6 +536,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.packedNodes = k->packed_nodes;
     a.packedTris = k->packed_tris;
     a.skips = k->packed_skips;
+    a.octNodes = k->oct_nodes;
+    a.leafExt = reinterpret_cast<const uint2*>(k->leaf_ext);
     a.nNodes = k->n_nodes;
     a.nTris = k->n_tris;
     a.width = W;
@@ -482,14 +574,17 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.shadeMin = k->shade_min;
     a.stepWeightNode = k->w_node;
     a.stepWeightLeaf = k->w_leaf;
+    a.poolShadeMin = k->pool_shade;
+    a.parkMin = k->park_min;
+    a.lowWork = k->low_work;
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
 
-    // LDS: packed nodes (32 B) + triangles (48 B) + skip pointers (32 B per node); no stack
-    const size_t scene_bytes = (size_t)k->n_nodes * 64 + (size_t)k->n_tris * 48;
+    // LDS: octant node records (8 x 32 B per node) + triangles (48 B); no stack
+    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 48;
     const bool lds = !k->force_global && scene_bytes <= kLdsBudget;
-    const size_t smem = lds ? scene_bytes : 0;
+    const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;
@@ -577,7 +672,8 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
 
 int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (!k) return RT_INVALID_KERNEL;
-    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP) return RT_INVALID_VALUE;
+    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP && sched != RT_SCHED_POOL)
+        return RT_INVALID_VALUE;
     k->sched = sched;
     return RT_SUCCESS;
 }
@@ -661,6 +757,7 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     out->cycles_traverse = h[5];
     out->cycles_shade = h[6];
     out->cycles_total = h[7];
+    for (int i = 0; i < 12; ++i) out->sched[i] = h[8 + i];
     out->launches = k->launches;
     out->kernel_ms = k->kernel_ms;
     return RT_SUCCESS;

@@ -89,15 +89,19 @@ __device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, 
 }
 
 // ---- scene access ------------------------------------------------------------------------
-// Packed node: q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y, bmax.z, offset, meta),
-// meta = nPrimitives | axis << 16.  Packed triangle: p1, e1, e2 (w unused).
+// Global (HBM/L2) scenes: packed node q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y,
+// bmax.z, offset, meta), meta = nPrimitives | axis << 16, plus [node][octant] skip pointers.
+// LDS scenes: octant-resolved records [node][octant] = {near.xyz, far.x}, {far.yz, hit_next,
+// miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
 struct SceneView {
-    const float4* nodes;    // LDS or global
+    const float4* nodes;    // global path
     const float4* tris;     // LDS or global
-    const uint32_t* skips;  // [node][octant]: next node in this octant's DFS order after the subtree
+    const uint32_t* skips;  // global path: [node][octant] next node in the octant's DFS order
+    const float4* onodes;   // LDS path: octant-resolved node records
 };
 
 constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
+constexpr uint32_t kLeafBit = 0x80000000u, kLeafExtBit = 0x40000000u;
 
 // Scene into LDS once per workgroup (when it fits), else read in place.
 template <bool kLdsScene>
@@ -105,18 +109,18 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     if (kLdsScene) {
         const int tid = threadIdx.x;
-        float4* ln = smem;
-        float4* lt = smem + 2 * a.nNodes;
-        float4* lk = lt + 3 * a.nTris;
-        const float4* gk = reinterpret_cast<const float4*>(a.skips);
-        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) ln[i] = a.packedNodes[i];
+        float4* lo = smem;
+        float4* lt = smem + 16 * a.nNodes;
+        for (uint32_t i = tid; i < 16 * a.nNodes; i += 256) lo[i] = a.octNodes[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-        for (uint32_t i = tid; i < 2 * a.nNodes; i += 256) lk[i] = gk[i];
         __syncthreads();
-        return SceneView{ln, lt, reinterpret_cast<const uint32_t*>(lk)};
+        return SceneView{nullptr, lt, nullptr, lo};
     }
-    return SceneView{a.packedNodes, a.packedTris, a.skips};
+    return SceneView{a.packedNodes, a.packedTris, a.skips, nullptr};
 }
+
+// LDS floats of the scene (the pool schedule's per-wave pools follow it)
+__device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) { return 16u * a.nNodes + 3u * a.nTris; }
 
 struct Traversal {
     float t;
@@ -140,6 +144,54 @@ __device__ __forceinline__ bool ray_bounds(const float4 q0, const float4 q1, con
     t0 = __builtin_fmaxf(t0, (nz - r.o.z) * r.inv.z);
     t1 = __builtin_fminf(t1, (fz - r.o.z) * r.inv.z);
     return t1 >= t0;
+}
+
+// One node visit of kernel_bvh.cl:184-215: returns true when the ray enters a leaf (its
+// triangles [first, first + count) are tested next); `next` is the node the walk continues
+// at -- the near child of a passed interior node, else the octant's skip pointer.
+template <bool kOct>
+__device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                           float t, uint32_t& next, uint32_t& first, uint32_t& count) {
+    if (kOct) {
+        const uint32_t i = 2u * (8u * cur + r.sgn);
+        const float4 A = sc.onodes[i], B = sc.onodes[i + 1];
+        float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+        float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+        t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+        t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+        t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+        t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+        const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
+        const bool hit = t1 >= t0;
+        const bool leaf = hit && (hn & kLeafBit);
+        next = (hit && !leaf) ? hn : mn;
+        if (leaf) {
+            if (hn & kLeafExtBit) {
+                const uint2 e = a.leafExt[hn & ~(kLeafBit | kLeafExtBit)];
+                first = e.x;
+                count = e.y;
+            } else {
+                first = hn & 0x00ffffffu;
+                count = ((hn >> 24) & 0x3fu) + 1u;
+            }
+        }
+        return leaf;
+    }
+    const float4 q0 = sc.nodes[2 * cur];
+    const float4 q1 = sc.nodes[2 * cur + 1];
+    next = sc.skips[8 * cur + r.sgn];
+    if (ray_bounds(q0, q1, r, t)) {
+        const uint32_t off = __float_as_uint(q1.z);
+        const uint32_t meta = __float_as_uint(q1.w);
+        const uint32_t np = meta & 0xffffu;
+        if (np > 0) {
+            first = off;
+            count = np;
+            return true;
+        }
+        next = ((r.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
+    }
+    return false;
 }
 
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.
@@ -171,32 +223,21 @@ __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, con
 // a node whose box is missed -- or finishing a leaf -- continues at skip[node][octant], the
 // node the reference pops next; a passed interior node continues at its near child
 // (the second child when sign[axis], kernel_bvh.cl:200-207).
-template <class M, bool kStats>
-__device__ __forceinline__ Traversal intersect(const SceneView& sc, const Ray& r, uint32_t& visits,
-                                               uint32_t& tests) {
+template <class M, bool kOct, bool kStats>
+__device__ __forceinline__ Traversal intersect(const SceneView& sc, const KernelArgs& a, const Ray& r,
+                                               uint32_t& visits, uint32_t& tests) {
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
     uint32_t cur = 0;
     while (cur != kEnd) {
-        const float4 q0 = sc.nodes[2 * cur];
-        const float4 q1 = sc.nodes[2 * cur + 1];
-        const uint32_t skip = sc.skips[8 * cur + r.sgn];
         if (kStats) ++visits;
-        if (ray_bounds(q0, q1, r, h.t)) {
-            const uint32_t off = __float_as_uint(q1.z);
-            const uint32_t meta = __float_as_uint(q1.w);
-            const uint32_t np = meta & 0xffffu;
-            if (np > 0) {
-                for (uint32_t i = 0; i < np; ++i) {
-                    if (kStats) ++tests;
-                    ray_triangle<M>(sc.tris + 3 * (size_t)(off + i), (int32_t)(off + i), r, h);
-                }
-                cur = skip;
-            } else {
-                cur = ((r.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
+        uint32_t next, first = 0, count = 0;
+        if (node_visit<kOct>(sc, a, cur, r, h.t, next, first, count)) {
+            for (uint32_t i = 0; i < count; ++i) {
+                if (kStats) ++tests;
+                ray_triangle<M>(sc.tris + 3 * (size_t)(first + i), (int32_t)(first + i), r, h);
             }
-        } else {
-            cur = skip;
         }
+        cur = next;
     }
     return h;
 }
@@ -324,7 +365,7 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
 }
 
 // kernel_bvh.cl:349-384 (Render)
-template <class M, bool kStats>
+template <class M, bool kOct, bool kStats>
 __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* __restrict__ tris_full,
                                      const rt_cl_material* __restrict__ mats, Ray ray,
                                      uint32_t& seed, const KernelArgs& a,
@@ -333,7 +374,7 @@ __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* 
     const uint32_t bounces = (uint32_t)a.lightBounces;
     for (uint32_t i = 0; i < bounces; ++i) {
         if (kStats) ++st.rays;
-        const Traversal h = intersect<M, kStats>(sc, ray, st.visits, st.tests);
+        const Traversal h = intersect<M, kOct, kStats>(sc, a, ray, st.visits, st.tests);
         if (i == 0) {
             prim_id = h.prim;
             prim_t = h.t;
@@ -345,8 +386,7 @@ __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* 
 
 // kernel_bvh.cl:449-455: write (frameCount 0) or gamma-accumulate one work-item's result.
 template <class M>
-__device__ __forceinline__ void finish_pixel(const KernelArgs& a, uint32_t gid, F3 rad, int32_t pid,
-                                             float pt) {
+__device__ __forceinline__ void finish_color(const KernelArgs& a, uint32_t gid, F3 rad) {
     F3 out;
     if (a.frameCount == 0) {
         out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
@@ -358,6 +398,12 @@ __device__ __forceinline__ void finish_pixel(const KernelArgs& a, uint32_t gid, 
         out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
     }
     a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
+}
+
+template <class M>
+__device__ __forceinline__ void finish_pixel(const KernelArgs& a, uint32_t gid, F3 rad, int32_t pid,
+                                             float pt) {
+    finish_color<M>(a, gid, rad);
     if (a.hitIds) {
         a.hitIds[gid] = pid;
         a.hitT[gid] = pt;
@@ -411,7 +457,7 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
         const Ray ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
         int32_t pid = -1;
         float pt = 0.0f;
-        const F3 rad = render<M, kStats>(sc, a.trisFull, a.materials, ray, seed, a, pid, pt, st);
+        const F3 rad = render<M, kLdsScene, kStats>(sc, a.trisFull, a.materials, ray, seed, a, pid, pt, st);
         finish_pixel<M>(a, gid, rad, pid, pt);
     }
     if (kStats) flush_stats(a, st, lane);
@@ -500,7 +546,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
         // ---- one bounce of every live path -------------------------------------------------
         if (active) {
             if (kStats) ++st.rays;
-            const Traversal h = intersect<M, kStats>(sc, ray, st.visits, st.tests);
+            const Traversal h = intersect<M, kLdsScene, kStats>(sc, a, ray, st.visits, st.tests);
             if (bounce == 0u) {
                 pid = h.prim;
                 pt = h.t;
@@ -566,12 +612,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
+    // diagnostic lane-utilisation counters (wave-uniform): steps / rounds and lanes served
+    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
+             u_rrounds = 0, u_rlanes = 0, u_other = 0, u_shadew = 0, u_freew = 0, u_pad = 0;
 
     for (;;) {
         // ---- finish + refill: accumulate finished paths, start new pixels ----------------------
         uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t n_free = popc_ballot(state == kIdle || state == kDone);
         if (n_free == 64u || (!exhausted && n_free >= kRefillMin)) {
+            if (kStats) {
+                ++u_rrounds;
+                u_rlanes += n_free;
+            }
             if (state == kDone) {
                 finish_pixel<M>(a, gid, radiance, pid, pt);
                 state = kIdle;
@@ -644,24 +697,26 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (popc_ballot(state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
+            if (kStats) {
+                u_shadew += popc_ballot(state == kShade);
+                u_freew += popc_ballot(state == kIdle || state == kDone);
+                u_other += leaf_step ? n_trav : n_leaf;
+                if (leaf_step) {
+                    ++u_tsteps;
+                    u_tlanes += n_leaf;
+                } else {
+                    ++u_nsteps;
+                    u_nlanes += n_trav;
+                }
+            }
             if (!leaf_step) {
                 if (state == kTrav) {
-                    const float4 q0 = sc.nodes[2 * cur];
-                    const float4 q1 = sc.nodes[2 * cur + 1];
-                    const uint32_t skip = sc.skips[8 * cur + ray.sgn];
                     if (kStats) ++st.visits;
-                    uint32_t next = skip;
-                    if (ray_bounds(q0, q1, ray, h.t)) {
-                        const uint32_t off = __float_as_uint(q1.z);
-                        const uint32_t meta = __float_as_uint(q1.w);
-                        const uint32_t np = meta & 0xffffu;
-                        if (np > 0) {
-                            state = kLeaf;
-                            leaf_i = off;
-                            leaf_end = off + np;
-                        } else {
-                            next = ((ray.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
-                        }
+                    uint32_t next, first = 0, count = 0;
+                    if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
+                        state = kLeaf;
+                        leaf_i = first;
+                        leaf_end = first + count;
                     }
                     cur = next;
                     if (state == kTrav && next == kEnd) state = kShade;
@@ -678,7 +733,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 
         // ---- shading ---------------------------------------------------------------------------
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats) cyc_trav += tC - tB;
+        if (kStats) {
+            cyc_trav += tC - tB;
+            const uint32_t ns = popc_ballot(state == kShade);
+            if (ns) {
+                ++u_srounds;
+                u_slanes += ns;
+            }
+        }
         if (state == kShade) {
             if (bounce == 0u) {
                 pid = h.prim;
@@ -705,6 +767,18 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
             atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
             atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
+            atomicAdd(&a.stats[8], (unsigned long long)u_nsteps);
+            atomicAdd(&a.stats[9], (unsigned long long)u_nlanes);
+            atomicAdd(&a.stats[10], (unsigned long long)u_tsteps);
+            atomicAdd(&a.stats[11], (unsigned long long)u_tlanes);
+            atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
+            atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
+            atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
+            atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
+            atomicAdd(&a.stats[16], (unsigned long long)u_other);
+            atomicAdd(&a.stats[17], (unsigned long long)u_shadew);
+            atomicAdd(&a.stats[18], (unsigned long long)u_freew);
+            atomicAdd(&a.stats[19], (unsigned long long)u_pad);
         }
     }
 }
@@ -728,6 +802,415 @@ void kernel_entry_step_devicelib(KernelArgs a) {
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
     step_body<MathPinned, kLdsScene, kStats>(a);
+}
+
+// ---- pool schedule: per-wave LDS path pool, full-wave shading ------------------------------
+// The step schedule leaves a third of a wave idle during traversal at 9 bounces: lanes whose
+// traversal ended wait (up to the shading threshold) and freed lanes wait for a refill
+// batch (profiles/r01/phase_*.txt).  Here every wave owns a pool of 64 path records in LDS
+// (the "hit" or "continuation" of a path, 112 B slots) and three slot stacks:
+//   trace-ready -- a continuation ray produced by shading, waiting for a lane
+//   shade-ready -- a finished traversal (ray + {t, primitive, u, v}) waiting for shading
+//   free
+// A lane whose traversal ends parks its path as shade-ready -- exchanging it for a
+// continuation when one is waiting -- and keeps tracing; idle lanes take continuations, then
+// new camera rays.  Shading runs when 64 records are ready (a full wave), each lane
+// shading one record in registers separate from its own traversal state, and writes the
+// continuation back into the same slot (or accumulates the pixel when the path ends).
+// Per path the operations, their order and the RNG stream are the reference's, so every
+// pixel and hit is bit-identical to the other schedules.  No cross-wave communication:
+// the pool is wave-private, LDS ops of one wave execute in order, no barriers.
+constexpr uint32_t kFin = 3;  // pool schedule: traversal finished, waiting to be parked
+constexpr uint32_t kPoolSlots = 64;
+constexpr uint32_t kPoolChunks = 7;
+static_assert(kPoolWaveBytes == kPoolSlots * kPoolChunks * 16 + 3 * kPoolSlots * 4, "pool layout");
+
+struct PoolView {
+    float4* rec;       // [chunk][slot] float4
+    uint32_t* tstack;  // trace-ready slots
+    uint32_t* sstack;  // shade-ready slots
+    uint32_t* fstack;  // free slots
+};
+
+struct PathState {
+    uint32_t gid, seed, bounce;
+    F3 radiance, beta;
+};
+
+// shade-ready record: o, d, {t, prim, u, v}, path state
+__device__ __forceinline__ void pool_put_hit(const PoolView& p, uint32_t s, const Ray& r, const Traversal& h,
+                                             const PathState& ps) {
+    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, h.t, __int_as_float(h.prim));
+    p.rec[2 * kPoolSlots + s] = make_float4(h.u, h.v, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
+    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
+    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
+}
+
+__device__ __forceinline__ void pool_get_hit(const PoolView& p, uint32_t s, Ray& r, Traversal& h, PathState& ps) {
+    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
+                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
+    r.o = F3{c0.x, c0.y, c0.z};
+    r.d = F3{c0.w, c1.x, c1.y};
+    h = Traversal{c1.z, __float_as_int(c1.w), c2.x, c2.y};
+    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
+                   F3{c4.x, c4.y, c4.z}};
+}
+
+// trace-ready record: the initialised next ray (o, d, 1/d) and path state
+__device__ __forceinline__ void pool_put_ray(const PoolView& p, uint32_t s, const Ray& r, const PathState& ps) {
+    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
+    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, 0.0f, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
+    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
+    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
+}
+
+__device__ __forceinline__ void pool_get_ray(const PoolView& p, uint32_t s, Ray& r, PathState& ps) {
+    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
+                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
+    r.o = F3{c0.x, c0.y, c0.z};
+    r.d = F3{c0.w, c1.x, c1.y};
+    r.inv = F3{c1.z, c1.w, c2.x};
+    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
+    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
+                   F3{c4.x, c4.y, c4.z}};
+}
+
+// a lane's in-flight state (any lane state), parked in a slot during a shading round
+__device__ __forceinline__ void pool_put_lane(const PoolView& p, uint32_t s, uint32_t state, const Ray& r,
+                                              const Traversal& h, uint32_t cur, uint32_t leaf_i,
+                                              uint32_t leaf_end, const PathState& ps) {
+    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
+    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, h.t, __int_as_float(h.prim), h.u);
+    p.rec[3 * kPoolSlots + s] = make_float4(h.v, __uint_as_float(cur), __uint_as_float(leaf_i),
+                                            __uint_as_float(leaf_end));
+    p.rec[4 * kPoolSlots + s] = make_float4(__uint_as_float(state), __uint_as_float(ps.gid),
+                                            __uint_as_float(ps.seed), __uint_as_float(ps.bounce));
+    p.rec[5 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, ps.beta.x);
+    p.rec[6 * kPoolSlots + s] = make_float4(ps.beta.y, ps.beta.z, 0.0f, 0.0f);
+}
+
+__device__ __forceinline__ void pool_get_lane(const PoolView& p, uint32_t s, uint32_t& state, Ray& r,
+                                              Traversal& h, uint32_t& cur, uint32_t& leaf_i, uint32_t& leaf_end,
+                                              PathState& ps) {
+    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
+                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s], c5 = p.rec[5 * kPoolSlots + s],
+                 c6 = p.rec[6 * kPoolSlots + s];
+    r.o = F3{c0.x, c0.y, c0.z};
+    r.d = F3{c0.w, c1.x, c1.y};
+    r.inv = F3{c1.z, c1.w, c2.x};
+    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
+    h = Traversal{c2.y, __float_as_int(c2.z), c2.w, c3.x};
+    cur = __float_as_uint(c3.y);
+    leaf_i = __float_as_uint(c3.z);
+    leaf_end = __float_as_uint(c3.w);
+    state = __float_as_uint(c4.x);
+    ps = PathState{__float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w), F3{c5.x, c5.y, c5.z},
+                   F3{c5.w, c6.x, c6.y}};
+}
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <class M, bool kLdsScene, bool kStats>
+__device__ __forceinline__ void pool_body(const KernelArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int tid = threadIdx.x;
+    const SceneView sc = stage_scene<kLdsScene>(a);
+    const uint32_t scene_f4 = kLdsScene ? lds_scene_f4(a) : 0u;
+    float4* region = smem + scene_f4 + (uint32_t)(tid >> 6) * (kPoolWaveBytes / 16u);
+    uint32_t* stacks = reinterpret_cast<uint32_t*>(region + kPoolChunks * kPoolSlots);
+    const PoolView pv{region, stacks, stacks + kPoolSlots, stacks + 2 * kPoolSlots};
+
+    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
+    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
+    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
+    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
+    const uint32_t fh = frame_hash(a.frameCount);
+    const uint32_t bounces = (uint32_t)a.lightBounces;
+    const uint32_t total = a.nTiles * 64u;
+    const uint32_t rowEnd = a.rowBegin + a.rowCount;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const uint32_t kRefillMin = a.refillMin;  // camera rays when this many lanes are idle
+    const uint32_t kShadeMin = a.poolShadeMin;  // shade when this many records are ready
+    const uint32_t kParkMin = a.parkMin;      // park when this many traversals have ended
+    const uint32_t kLowWork = a.lowWork;      // ... or shade early when tracing work runs low
+
+    pv.fstack[lane] = lane;
+    uint32_t nt = 0, ns = 0, ne = kPoolSlots;  // stack depths (wave-uniform)
+
+    LaneStats st;
+    uint32_t state = kIdle;
+    PathState ps{0u, 0u, 0u, f3s(0.0f), f3s(1.0f)};
+    Ray ray{};
+    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
+    uint32_t cur = 0, leaf_i = 0, leaf_end = 0;
+    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    bool exhausted = false;                    // wave-uniform
+    uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
+    const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
+             u_rrounds = 0, u_rlanes = 0, u_other = 0, u_finw = 0, u_idlew = 0, u_parks = 0;
+
+    for (;;) {
+        uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
+        // ---- park ended traversals: exchange for a continuation, else take a free slot -----
+        {
+            const unsigned long long fin = __ballot(state == kFin);
+            if (fin) {
+                const uint32_t nf = (uint32_t)__popcll(fin);
+                const uint32_t x = min(nf, nt), y = min(nf - x, ne);
+                if (kStats) u_parks += x + y;
+                if (state == kFin) {
+                    const uint32_t rank = lane_rank(fin);
+                    if (rank < x) {
+                        const uint32_t slot = pv.tstack[nt - 1u - rank];
+                        Ray nr;
+                        PathState nps;
+                        pool_get_ray(pv, slot, nr, nps);
+                        pool_put_hit(pv, slot, ray, h, ps);
+                        pv.sstack[ns + rank] = slot;
+                        ray = nr;
+                        ps = nps;
+                        state = kTrav;
+                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                        cur = 0;
+                    } else if (rank < x + y) {
+                        const uint32_t slot = pv.fstack[ne - 1u - (rank - x)];
+                        pool_put_hit(pv, slot, ray, h, ps);
+                        pv.sstack[ns + rank] = slot;
+                        state = kIdle;
+                    }
+                }
+                nt -= x;
+                ne -= y;
+                ns += x + y;
+            }
+        }
+        // ---- idle lanes take waiting continuations --------------------------------------------
+        {
+            const unsigned long long idle = __ballot(state == kIdle);
+            if (idle != 0ull && nt > 0u) {
+                const uint32_t x = min((uint32_t)__popcll(idle), nt);
+                if (state == kIdle) {
+                    const uint32_t rank = lane_rank(idle);
+                    if (rank < x) {
+                        const uint32_t slot = pv.tstack[nt - 1u - rank];
+                        pool_get_ray(pv, slot, ray, ps);
+                        pv.fstack[ne + rank] = slot;
+                        state = kTrav;
+                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                        cur = 0;
+                    }
+                }
+                nt -= x;
+                ne += x;
+            }
+        }
+        // ---- new pixels (camera rays) for idle lanes -------------------------------------------
+        {
+            const uint32_t n_idle = popc_ballot(state == kIdle);
+            const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
+            if (!exhausted && n_idle > 0u && (n_idle >= kRefillMin || n_act == 0u)) {
+                if (kStats) {
+                    ++u_rrounds;
+                    u_rlanes += n_idle;
+                }
+                while (!exhausted) {
+                    const unsigned long long idle = __ballot(state == kIdle);
+                    if (idle == 0ull) break;
+                    if (chunk_used >= 64u) {
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(a.workCounter, 64u);
+                        b = __shfl(b, 0, 64);
+                        if (b >= total) {
+                            exhausted = true;
+                            break;
+                        }
+                        chunk_base = b;
+                        chunk_used = 0;
+                    }
+                    const uint32_t rank = lane_rank(idle);
+                    const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+                    if (state == kIdle && rank < take) {
+                        const uint32_t idx = chunk_base + chunk_used + rank;
+                        const uint32_t tile = idx >> 6, w = idx & 63u;
+                        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+                        const uint32_t x = tx * 8u + (w & 7u),
+                                       row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
+                        const uint64_t g64 = (uint64_t)row * a.width + x;
+                        if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
+                            ps.gid = (uint32_t)g64;
+                            ps.seed = ps.gid + fh;  // kernel_bvh.cl:445
+                            ray = create_ray<M>(ps.gid, a.width, a.height, camPos, camFront, camUp, angle, ps.seed);
+                            ps.radiance = f3s(0.0f);
+                            ps.beta = f3s(1.0f);
+                            ps.bounce = 0;
+                            if (bounces > 0u) {
+                                state = kTrav;
+                                h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                                cur = 0;
+                                if (kStats) ++st.rays;
+                            } else {
+                                finish_pixel<M>(a, ps.gid, f3s(0.0f), -1, 0.0f);  // no bounce: radiance 0
+                            }
+                        }
+                    }
+                    chunk_used += take;
+                }
+            }
+        }
+        uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
+        if (kStats) cyc_refill += tB - tA;
+        // ---- shading: one record per lane, a full wave when the pool is full ------------------
+        // Only with no continuation waiting (nt == 0): then every lane owns a slot for the
+        // round -- its shade-ready record's, or a free one -- and parks its own in-flight state
+        // there while it shades, so the traversal registers are free for the shading code.
+        const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
+        if (nt == 0u && (ns >= kShadeMin || (ns > 0u && n_act < kLowWork))) {
+            const uint32_t nb = ns;  // <= 64; ne == 64 - nb
+            if (kStats) {
+                ++u_srounds;
+                u_slanes += nb;
+            }
+            const bool mine = lane < nb;
+            const uint32_t slot = mine ? pv.sstack[nb - 1u - lane] : pv.fstack[ne - 1u - (lane - nb)];
+            Ray sr;
+            Traversal sh;
+            PathState sp;
+            // Every lane runs the shading code (a lane without a record shades a miss and
+            // discards it): no divergent region around the large shading body, which keeps
+            // the register allocation of this loop close to the step schedule's.
+            pool_get_hit(pv, slot, sr, sh, sp);
+            if (!mine) sh.prim = -1;
+            pool_put_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
+            // compiler-only fences: keep the spill and the reload real (no store-to-load
+            // forwarding of the parked state across the shading code)
+            __asm__ volatile("" ::: "memory");
+            if (mine && sp.bounce == 0u && a.hitIds) {
+                a.hitIds[sp.gid] = sh.prim;
+                a.hitT[sp.gid] = sh.t;
+            }
+            LaneStats sst;
+            const bool more = shade_bounce<M, kStats>(sh, sr, sp.radiance, sp.beta, sp.seed, a.trisFull,
+                                                      a.materials, a, sst);
+            if (kStats && mine) st.hits += sst.hits;
+            ++sp.bounce;
+            const bool cont = mine && more && sp.bounce < bounces;
+            if (mine && !cont) {
+                finish_color<M>(a, sp.gid, F3{M::max(sp.radiance.x, 0.0f), M::max(sp.radiance.y, 0.0f),
+                                              M::max(sp.radiance.z, 0.0f)});
+            }
+            if (kStats && cont) ++st.rays;
+            __asm__ volatile("" ::: "memory");
+            pool_get_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
+            const unsigned long long cm = __ballot(cont);
+            const unsigned long long fm = __ballot(mine && !cont);
+            if (cont) {
+                pool_put_ray(pv, slot, sr, sp);
+                pv.tstack[lane_rank(cm)] = slot;
+            } else if (mine) {
+                pv.fstack[ne + lane_rank(fm)] = slot;
+            }
+            nt = (uint32_t)__popcll(cm);
+            ne += (uint32_t)__popcll(fm);
+            ns = 0;
+            if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tB;
+        }
+        if (n_act == 0u) {
+            if (exhausted && ns == 0u && nt == 0u && __ballot(state == kFin) == 0ull) break;
+            continue;
+        }
+
+        // ---- traversal steps (as in the step schedule) ----------------------------------------
+        for (;;) {
+            const uint32_t n_trav = popc_ballot(state == kTrav);
+            const uint32_t n_leaf = popc_ballot(state == kLeaf);
+            const uint32_t n_fin = popc_ballot(state == kFin);
+            if (n_trav + n_leaf == 0u) break;
+            if (n_fin >= kParkMin) break;
+            const uint32_t n_idle = 64u - n_trav - n_leaf - n_fin;
+            if (n_idle >= kRefillMin && (nt > 0u || !exhausted)) break;
+            if (nt == 0u && ns > 0u && n_trav + n_leaf < kLowWork) break;
+            const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
+            if (kStats) {
+                u_finw += n_fin;
+                u_idlew += n_idle;
+                u_other += leaf_step ? n_trav : n_leaf;
+                if (leaf_step) {
+                    ++u_tsteps;
+                    u_tlanes += n_leaf;
+                } else {
+                    ++u_nsteps;
+                    u_nlanes += n_trav;
+                }
+            }
+            if (!leaf_step) {
+                if (state == kTrav) {
+                    if (kStats) ++st.visits;
+                    uint32_t next, first = 0, count = 0;
+                    if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
+                        state = kLeaf;
+                        leaf_i = first;
+                        leaf_end = first + count;
+                    }
+                    cur = next;
+                    if (state == kTrav && next == kEnd) state = kFin;
+                }
+            } else {
+                if (state == kLeaf) {
+                    if (kStats) ++st.tests;
+                    ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                    ++leaf_i;
+                    if (leaf_i == leaf_end) state = cur == kEnd ? kFin : kTrav;
+                }
+            }
+        }
+        if (kStats) cyc_trav += __builtin_amdgcn_s_memtime() - tB;
+    }
+    if (kStats) {
+        flush_stats(a, st, (int)lane);
+        if (lane == 0) {
+            atomicAdd(&a.stats[4], (unsigned long long)cyc_refill);
+            atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
+            atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
+            atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
+            atomicAdd(&a.stats[8], (unsigned long long)u_nsteps);
+            atomicAdd(&a.stats[9], (unsigned long long)u_nlanes);
+            atomicAdd(&a.stats[10], (unsigned long long)u_tsteps);
+            atomicAdd(&a.stats[11], (unsigned long long)u_tlanes);
+            atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
+            atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
+            atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
+            atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
+            atomicAdd(&a.stats[16], (unsigned long long)u_other);
+            atomicAdd(&a.stats[17], (unsigned long long)u_finw);
+            atomicAdd(&a.stats[18], (unsigned long long)u_idlew);
+            atomicAdd(&a.stats[19], (unsigned long long)u_parks);
+        }
+    }
+}
+
+#ifdef RT_POOL_DEVICELIB_WAVES
+#define RT_POOL_DEVICELIB_OCC __attribute__((amdgpu_waves_per_eu(RT_POOL_DEVICELIB_WAVES, 8)))
+#else
+#define RT_POOL_DEVICELIB_OCC
+#endif
+#ifdef RT_POOL_PINNED_WAVES
+#define RT_POOL_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_POOL_PINNED_WAVES, 8)))
+#else
+#define RT_POOL_PINNED_OCC
+#endif
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) RT_POOL_DEVICELIB_OCC void kernel_entry_pool_devicelib(KernelArgs a) {
+    pool_body<MathDeviceLib, kLdsScene, kStats>(a);
+}
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) RT_POOL_PINNED_OCC void kernel_entry_pool_pinned(KernelArgs a) {
+    pool_body<MathPinned, kLdsScene, kStats>(a);
 }
 
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
@@ -764,6 +1247,10 @@ static KernelFn pick_sched(int sched) {
     if (sched == kSchedStep) {
         if (M::kId == MathDeviceLib::kId) return kernel_entry_step_devicelib<L, S>;
         return kernel_entry_step_pinned<L, S>;
+    }
+    if (sched == kSchedPool) {
+        if (M::kId == MathDeviceLib::kId) return kernel_entry_pool_devicelib<L, S>;
+        return kernel_entry_pool_pinned<L, S>;
     }
     return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
 }

@@ -17,6 +17,8 @@ struct KernelArgs {
     const float4* packedNodes;          // derived from slot 2: 2 x float4 per node
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
     const uint32_t* skips;              // derived from slot 2: [node][octant] DFS skip pointers
+    const float4* octNodes;             // derived from slot 2: [node][octant] resolved records (LDS path)
+    const uint2* leafExt;               // {first, count} of leaves the octant records cannot encode
     uint32_t nNodes, nTris;
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)
@@ -30,6 +32,7 @@ struct KernelArgs {
     uint32_t refillMin, shadeMin;       // step schedule batching thresholds (lanes)
     uint32_t stepWeightNode, stepWeightLeaf;  // step schedule: relative cost of node / triangle steps
     uint32_t bandPeriod, bandPhase;     // 8-row bands: this launch renders bands b % period == phase
+    uint32_t poolShadeMin, parkMin, lowWork;  // pool schedule thresholds (records / lanes)
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
@@ -39,6 +42,10 @@ struct KernelArgs {
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
 constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
 constexpr int kSchedStep = 2;   // per-wave state machine: node / triangle steps, batched shading
+constexpr int kSchedPool = 3;   // step traversal + per-wave LDS path pool, full-wave shading
+constexpr int kNumSched = 4;
+// pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
+constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);

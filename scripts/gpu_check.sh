@@ -40,6 +40,10 @@ for step in "$@"; do
     dist2) run dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --math devicelib ;;
     benchbunny) run bench_bunny 600 python bench.py --scene bunny --no-cpu-baseline --steps 3 ;;
     phase) run phase 300 python scripts/phase_profile.py ;;
+    phasepool) run phase_pool 300 python scripts/phase_profile.py step pool ;;
+    poolpar) run pool_parity 600 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "schedules or interleaved" ;;
+    benchpool) run bench_pool_dl 600 python bench.py --sched pool --no-cpu-baseline && \
+               run bench_pool_pin 600 python bench.py --sched pool --math pinned --no-cpu-baseline ;;
     refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline && \
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;

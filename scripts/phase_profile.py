@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase wave-cycle shares of the step schedule (stats variant, s_memtime)."""
+"""Diagnostic: per-phase wave-cycle shares of the step / pool schedules (stats variant, s_memtime).
+Usage: phase_profile.py [step|pool ...]"""
 import os
 import sys
 
@@ -11,15 +12,25 @@ from clrt import _native as N  # noqa: E402
 from hip_helpers import HipRenderer  # noqa: E402
 
 sc = clrt.scene.cornell()
-for math in (N.MATH_DEVICELIB, N.MATH_PINNED):
+scheds = sys.argv[1:] or ["step"]
+for name in scheds:
+  sched = {"step": N.SCHED_STEP, "pool": N.SCHED_POOL}[name]
+  for math in (N.MATH_DEVICELIB, N.MATH_PINNED):
     for lb in (1, 9):
-        r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=N.SCHED_STEP)
+        r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=sched)
         r.frame(1, light_bounces=lb)
         r.ctx.Finish()
         s = r.k.stats()
         c = s["cycles"]
         tot = c["total"] or 1
-        print(f"math={math} lb={lb} rays={s['rays']} visits={s['node_visits']} tests={s['tri_tests']} "
+        u = s["sched"]
+        print(f"{name} math={math} lb={lb} rays={s['rays']} visits={s['node_visits']} tests={s['tri_tests']} "
               f"| refill {c['refill']/tot:.3f} traverse {c['traverse']/tot:.3f} shade {c['shade']/tot:.3f} "
-              f"| cycles/ray {tot/ s['rays'] * 1.0:.0f} (sum over waves)")
+              f"| lanes/step node {u['node_lanes']/max(1,u['node_steps']):.1f} ({u['node_steps']}) "
+              f"tri {u['tri_lanes']/max(1,u['tri_steps']):.1f} ({u['tri_steps']}) "
+              f"shade {u['shade_lanes']/max(1,u['shade_rounds']):.1f} ({u['shade_rounds']}) "
+              f"refill {u['refill_lanes']/max(1,u['refill_rounds']):.1f} ({u['refill_rounds']}) "
+              f"| per step: other {u['other_lanes']/max(1,u['node_steps']+u['tri_steps']):.1f} "
+              f"shade-wait {u['shade_wait']/max(1,u['node_steps']+u['tri_steps']):.1f} "
+              f"free {u['free_wait']/max(1,u['node_steps']+u['tri_steps']):.1f}")
         r.close()

@@ -114,9 +114,10 @@ def test_frame_count_zero_path(cornell, oracle_mod):
 
 @pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB])
 def test_schedules_agree_bit_exact(cornell, math):
-    """Tile schedule and path-regeneration schedule compute identical pixels and counters."""
+    """Every schedule (tiles, path regeneration, step, LDS path pool) computes identical pixels,
+    primary hits and counters."""
     outs = []
-    for sched in (N.SCHED_TILES, N.SCHED_REGEN, N.SCHED_STEP):
+    for sched in (N.SCHED_TILES, N.SCHED_REGEN, N.SCHED_STEP, N.SCHED_POOL):
         r = HipRenderer(cornell, 301, 157, math=math, hits=True, stats=True, sched=sched)
         for f in (1, 2, 3):
             r.frame(f, light_bounces=9)
@@ -167,12 +168,13 @@ def test_row_tiles_compose_to_full_frame(cornell):
     _assert_bits(a, b, "tiled")
 
 
-@pytest.mark.parametrize("sched", [N.SCHED_STEP, N.SCHED_REGEN])
+@pytest.mark.parametrize("sched", [N.SCHED_STEP, N.SCHED_REGEN, N.SCHED_POOL])
 def test_interleaved_bands_compose_full_frame(cornell, sched):
     """Multi-GPU sharding on one device: period-3 band interleave, each phase launched in
     turn (frames 1 and 2), equals the unsharded render; pack -> unpack round trip too."""
     import torch
     from clrt import multigpu as mg
+    torch.zeros(1, device="cuda:0")  # initialise torch's HIP context before the library's
     W, H, P = 203, 75, 3
     full = HipRenderer(cornell, W, H, sched=sched)
     for f in (1, 2):
@@ -253,3 +255,29 @@ def test_malformed_bvh_is_rejected_not_run(cornell):
         r.frame(1, light_bounces=1)
     assert e.value.code == -38
     r.close()
+
+
+def test_large_leaf_uses_leaf_table(cornell, oracle_mod):
+    """A root-only BVH -- one leaf holding all 72 triangles, more than the LDS node records
+    encode inline (64) -- takes the leaf-table path; bit-exact against the oracle."""
+    import dataclasses
+    tris = cornell.triangles
+    p = np.concatenate([tris["v1"]["position"], tris["v2"]["position"], tris["v3"]["position"]])[:, :3]
+    root = np.zeros(1, N.NODE_DTYPE)
+    root["bmin"][0, :3] = p.min(0)
+    root["bmax"][0, :3] = p.max(0)
+    root["nPrimitives"] = len(tris)
+    assert len(tris) > 64
+    sc = dataclasses.replace(cornell, nodes=root)
+    W, H = 96, 64
+    r = HipRenderer(sc, W, H, hits=True, stats=True)
+    r.frame(1, light_bounces=4)
+    got = r.result()
+    ids, _ = r.hits()
+    st = r.k.stats()
+    assert r.k.scene_in_lds()
+    r.close()
+    want, wids, _, c = _oracle(oracle_mod, sc, W, H, [1], 4, hits=True)
+    assert np.array_equal(ids, wids)
+    _assert_bits(rgb(got), rgb(want), "root-leaf radiance")
+    assert (st["node_visits"], st["tri_tests"]) == (c["node_visits"], c["tri_tests"])
