@@ -89,8 +89,8 @@ struct rt_kernel_s {
     float4* packed_tris = nullptr;
     uint32_t* packed_skips = nullptr;
     float4* oct_nodes = nullptr;       // [node][octant] 2 x float4 (LDS-resident scenes)
-    uint32_t* leaf_ext = nullptr;      // {first, count} of leaves the octant records cannot encode
-    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0, leaf_ext_cap = 0;
+    bool oct_ok = false;               // every leaf fits the records' inline {first, count}
+    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
@@ -169,15 +169,17 @@ void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& sk
 //   A = {near.x, near.y, near.z, far.x}, B = {far.y, far.z, hit_next, miss_next}
 // where near/far are the slab planes kernel_bvh.cl:156-169 selects by the ray's signs
 // (bit-exact copies of pmin/pmax), miss_next = skip[n][o] and hit_next is the near child
-// (interior) or the leaf {first, count}: bit 31 set, then either count-1 (6 bits) and
-// first (24 bits), or bit 30 + an index into leaf_ext for leaves outside those ranges.
-// A node step is then two b128 reads, the slab arithmetic and one select.
-constexpr uint32_t kLeafBit = 0x80000000u, kLeafExtBit = 0x40000000u;
+// (interior) or the leaf {first, count}: bit 31 set, count-1 in bits 24-29 and first in
+// bits 0-23.  A node step is then two b128 reads, the slab arithmetic and one select.
+// Returns false when a leaf does not fit (> 64 primitives or first >= 2^24): such a
+// scene is rendered from the global layout instead (LDS scenes are small, so this takes
+// an unusual hand-made BVH).
+constexpr uint32_t kLeafBit = 0x80000000u;
 
-void build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
-                     std::vector<uint32_t>& out, std::vector<uint32_t>& ext) {
+bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
+                     std::vector<uint32_t>& out) {
     out.assign((size_t)n * 8 * 8, 0u);
-    ext.clear();
+    bool ok = true;
     auto bits = [](float f) {
         uint32_t u;
         std::memcpy(&u, &f, 4);
@@ -187,13 +189,10 @@ void build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
         const rt_cl_bvh_node& x = nd[i];
         uint32_t leaf = 0;
         if (x.nPrimitives > 0) {
-            if (x.offset < (1u << 24) && x.nPrimitives <= 64) {
+            if (x.offset < (1u << 24) && x.nPrimitives <= 64)
                 leaf = kLeafBit | ((uint32_t)(x.nPrimitives - 1) << 24) | x.offset;
-            } else {
-                leaf = kLeafBit | kLeafExtBit | (uint32_t)(ext.size() / 2);
-                ext.push_back(x.offset);
-                ext.push_back(x.nPrimitives);
-            }
+            else
+                ok = false;
         }
         const float lo[3] = {x.bounds.pmin.x, x.bounds.pmin.y, x.bounds.pmin.z};
         const float hi[3] = {x.bounds.pmax.x, x.bounds.pmax.y, x.bounds.pmax.z};
@@ -215,6 +214,7 @@ void build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
             r[7] = skips[(size_t)i * 8 + o];
         }
     }
+    return ok;
 }
 
 template <class T>
@@ -268,28 +268,21 @@ int prepare_scene(rt_kernel k) {
     }
     if (k->packed_skips_cap < (size_t)nn) {
         if (k->packed_skips) (void)hipFree(k->packed_skips);
-    if (k->oct_nodes) (void)hipFree(k->oct_nodes);
-    if (k->leaf_ext) (void)hipFree(k->leaf_ext);
         k->packed_skips = nullptr;
         k->packed_skips_cap = 0;
         hipError_t e = hipMalloc(&k->packed_skips, (size_t)nn * 8 * sizeof(uint32_t));
         if (e != hipSuccess) return map_hip(e);
         k->packed_skips_cap = nn;
     }
-    std::vector<uint32_t> oct, ext;
-    build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct, ext);
+    std::vector<uint32_t> oct;
+    const bool oct_ok = build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct);
     rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)nn * 16);
-    if (rc) return rc;
-    rc = ensure_dev(k->leaf_ext, k->leaf_ext_cap, std::max<size_t>(2, ext.size()));
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->packed_skips, skips.data(), skips.size() * sizeof(uint32_t),
                                       hipMemcpyHostToDevice, k->ctx->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                               k->ctx->stream);
-        if (e == hipSuccess && !ext.empty())
-            e = hipMemcpyAsync(k->leaf_ext, ext.data(), ext.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                                k->ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
         if (e != hipSuccess) return map_hip(e);
@@ -310,6 +303,7 @@ int prepare_scene(rt_kernel k) {
     k->n_tris = nt;
     k->n_mats = nmat;
     k->depth = depth;
+    k->oct_ok = oct_ok;
     k->packed_for_tris = tm;
     k->packed_tris_gen = tm->generation;
     k->packed_for_nodes = nm;
@@ -479,7 +473,6 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->packed_skips) (void)hipFree(k->packed_skips);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
-    if (k->leaf_ext) (void)hipFree(k->leaf_ext);
     if (k->dstats) (void)hipFree(k->dstats);
     if (k->work_counter) (void)hipFree(k->work_counter);
     delete k;
@@ -537,7 +530,6 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.packedTris = k->packed_tris;
     a.skips = k->packed_skips;
     a.octNodes = k->oct_nodes;
-    a.leafExt = reinterpret_cast<const uint2*>(k->leaf_ext);
     a.nNodes = k->n_nodes;
     a.nTris = k->n_tris;
     a.width = W;
@@ -583,7 +575,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
 
     // LDS: octant node records (8 x 32 B per node) + triangles (48 B); no stack
     const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 48;
-    const bool lds = !k->force_global && scene_bytes <= kLdsBudget;
+    const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0);
     k->last_lds = lds;
 

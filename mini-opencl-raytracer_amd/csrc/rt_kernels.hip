@@ -101,7 +101,7 @@ struct SceneView {
 };
 
 constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
-constexpr uint32_t kLeafBit = 0x80000000u, kLeafExtBit = 0x40000000u;
+constexpr uint32_t kLeafBit = 0x80000000u;  // octant record hit_next: leaf {first, count}
 
 // Scene into LDS once per workgroup (when it fits), else read in place.
 template <bool kLdsScene>
@@ -165,16 +165,8 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
         const bool hit = t1 >= t0;
         const bool leaf = hit && (hn & kLeafBit);
         next = (hit && !leaf) ? hn : mn;
-        if (leaf) {
-            if (hn & kLeafExtBit) {
-                const uint2 e = a.leafExt[hn & ~(kLeafBit | kLeafExtBit)];
-                first = e.x;
-                count = e.y;
-            } else {
-                first = hn & 0x00ffffffu;
-                count = ((hn >> 24) & 0x3fu) + 1u;
-            }
-        }
+        first = hn & 0x00ffffffu;
+        count = ((hn >> 24) & 0x3fu) + 1u;
         return leaf;
     }
     const float4 q0 = sc.nodes[2 * cur];
@@ -194,7 +186,11 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
     return false;
 }
 
-// kernel_bvh.cl:98-153 (RayTriangle), accept test only.
+// kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
+// early returns (det, u, v) become one accept predicate.  The values computed are the
+// ones the reference computes where it reaches them; the rest are discarded.  A wave
+// tests ~25 lanes' triangles at once and nearly always has some lane past every early
+// return, so the branches saved no arithmetic and cost exec-mask bookkeeping.
 template <class M>
 __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
                                              Traversal& h) {
@@ -202,16 +198,15 @@ __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, con
     const F3 p1{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
     const F3 pvec = M::cross(r.d, e2);
     const float det = M::dot(e1, pvec);
-    if (det < kHitEps) return;  // == (det < 1e-8 || -det > 1e-8); NaN falls through
     const float inv_det = 1.0f / det;
     const F3 tvec = r.o - p1;
     const float u = M::dot(tvec, pvec) * inv_det;
-    if (u < 0.0f || u > 1.0f) return;
     const F3 qvec = M::cross(tvec, e1);
     const float v = M::dot(r.d, qvec) * inv_det;
-    if (v < 0.0f || u + v > 1.0f) return;
     const float t = M::dot(e2, qvec) * inv_det;
-    if (t < h.t) {
+    // (det < 1e-8 || -det > 1e-8) == det < 1e-8 (NaN falls through, as in the reference)
+    const bool ok = !(det < kHitEps) & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) & !(u + v > 1.0f) & (t < h.t);
+    if (ok) {
         h.t = t;
         h.prim = idx;
         h.u = u;
@@ -577,6 +572,14 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
 // at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
+// steps of the chosen kind per scheduling decision (thresholds are re-checked after each
+// burst): the per-step ballots and threshold tests cost about as much as a node visit
+#ifndef RT_NODE_BURST
+#define RT_NODE_BURST 6
+#endif
+#ifndef RT_TRI_BURST
+#define RT_TRI_BURST 2
+#endif
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
@@ -710,23 +713,29 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 }
             }
             if (!leaf_step) {
-                if (state == kTrav) {
-                    if (kStats) ++st.visits;
-                    uint32_t next, first = 0, count = 0;
-                    if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
-                        state = kLeaf;
-                        leaf_i = first;
-                        leaf_end = first + count;
+#pragma unroll
+                for (int rep = 0; rep < RT_NODE_BURST; ++rep) {
+                    if (state == kTrav) {
+                        if (kStats) ++st.visits;
+                        uint32_t next, first = 0, count = 0;
+                        if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
+                            state = kLeaf;
+                            leaf_i = first;
+                            leaf_end = first + count;
+                        }
+                        cur = next;
+                        if (state == kTrav && next == kEnd) state = kShade;
                     }
-                    cur = next;
-                    if (state == kTrav && next == kEnd) state = kShade;
                 }
             } else {
-                if (state == kLeaf) {
-                    if (kStats) ++st.tests;
-                    ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                    ++leaf_i;
-                    if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
+#pragma unroll
+                for (int rep = 0; rep < RT_TRI_BURST; ++rep) {
+                    if (state == kLeaf) {
+                        if (kStats) ++st.tests;
+                        ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                        ++leaf_i;
+                        if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
+                    }
                 }
             }
         }

@@ -18,7 +18,6 @@ struct KernelArgs {
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
     const uint32_t* skips;              // derived from slot 2: [node][octant] DFS skip pointers
     const float4* octNodes;             // derived from slot 2: [node][octant] resolved records (LDS path)
-    const uint2* leafExt;               // {first, count} of leaves the octant records cannot encode
     uint32_t nNodes, nTris;
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)

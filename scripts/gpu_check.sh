@@ -47,6 +47,10 @@ for step in "$@"; do
     refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline && \
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    variants) for m in devicelib pinned; do \
+                for v in mini-opencl-raytracer_amd/lib/variants/*.so; do n=$(basename $v .so); \
+                  RT_HIP_LIB=$v run ab_${n}_$m 300 python bench.py --math $m --no-cpu-baseline --steps 3 || exit $?; done; \
+                run ab_main_$m 300 python bench.py --math $m --no-cpu-baseline --steps 3 || exit $?; done ;;
     *) echo "unknown step $step" ;;
   esac
 done

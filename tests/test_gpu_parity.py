@@ -257,9 +257,9 @@ def test_malformed_bvh_is_rejected_not_run(cornell):
     r.close()
 
 
-def test_large_leaf_uses_leaf_table(cornell, oracle_mod):
+def test_large_leaf_uses_global_layout(cornell, oracle_mod):
     """A root-only BVH -- one leaf holding all 72 triangles, more than the LDS node records
-    encode inline (64) -- takes the leaf-table path; bit-exact against the oracle."""
+    encode inline (64) -- is rendered from the global layout; bit-exact against the oracle."""
     import dataclasses
     tris = cornell.triangles
     p = np.concatenate([tris["v1"]["position"], tris["v2"]["position"], tris["v3"]["position"]])[:, :3]
@@ -275,7 +275,7 @@ def test_large_leaf_uses_leaf_table(cornell, oracle_mod):
     got = r.result()
     ids, _ = r.hits()
     st = r.k.stats()
-    assert r.k.scene_in_lds()
+    assert not r.k.scene_in_lds()
     r.close()
     want, wids, _, c = _oracle(oracle_mod, sc, W, H, [1], 4, hits=True)
     assert np.array_equal(ids, wids)
