@@ -89,6 +89,9 @@ struct rt_kernel_s {
     float4* packed_tris = nullptr;
     uint32_t* packed_skips = nullptr;
     float4* oct_nodes = nullptr;       // [node][octant] 2 x float4 (LDS-resident scenes)
+    float4* shade_tris = nullptr;      // compact shading records (normals + mtlIndex)
+    float4* shade_mats = nullptr;      // compact materials
+    size_t shade_tris_cap = 0, shade_mats_cap = 0;
     bool oct_ok = false;               // every leaf fits the records' inline {first, count}
     size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
@@ -295,9 +298,14 @@ int prepare_scene(rt_kernel k) {
         if (e != hipSuccess) return map_hip(e);
         k->packed_tris_cap = nt;
     }
+    rc = ensure_dev(k->shade_tris, k->shade_tris_cap, (size_t)nt * 3);
+    if (rc) return rc;
+    rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 3);
+    if (rc) return rc;
     hipError_t e = rtk::launch_pack(static_cast<const rt_cl_bvh_node*>(nm->dptr), nn, k->packed_nodes,
                                     static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
-                                    k->ctx->stream);
+                                    k->shade_tris, static_cast<const rt_cl_material*>(mm->dptr), nmat,
+                                    k->shade_mats, k->ctx->stream);
     if (e != hipSuccess) return map_hip(e);
     k->n_nodes = nn;
     k->n_tris = nt;
@@ -473,6 +481,8 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->packed_skips) (void)hipFree(k->packed_skips);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
+    if (k->shade_tris) (void)hipFree(k->shade_tris);
+    if (k->shade_mats) (void)hipFree(k->shade_mats);
     if (k->dstats) (void)hipFree(k->dstats);
     if (k->work_counter) (void)hipFree(k->work_counter);
     delete k;
@@ -530,6 +540,9 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.packedTris = k->packed_tris;
     a.skips = k->packed_skips;
     a.octNodes = k->oct_nodes;
+    a.shadeTris = k->shade_tris;
+    a.shadeMats = k->shade_mats;
+    a.nMats = k->n_mats;
     a.nNodes = k->n_nodes;
     a.nTris = k->n_tris;
     a.width = W;
@@ -573,8 +586,9 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
 
-    // LDS: octant node records (8 x 32 B per node) + triangles (48 B); no stack
-    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 48;
+    // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
+    // (48 B per triangle, 48 B per material); no stack
+    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 48;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0);
     k->last_lds = lds;

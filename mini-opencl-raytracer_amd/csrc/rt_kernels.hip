@@ -98,6 +98,8 @@ struct SceneView {
     const float4* tris;     // LDS or global
     const uint32_t* skips;  // global path: [node][octant] next node in the octant's DFS order
     const float4* onodes;   // LDS path: octant-resolved node records
+    const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, -}, {n3, -}
+    const float4* smats;    // per material: {diffuse, roughness}, {specular, -}, {emission, -}
 };
 
 constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
@@ -110,17 +112,23 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     if (kLdsScene) {
         const int tid = threadIdx.x;
         float4* lo = smem;
-        float4* lt = smem + 16 * a.nNodes;
+        float4* lt = lo + 16 * a.nNodes;
+        float4* ls = lt + 3 * a.nTris;
+        float4* lm = ls + 3 * a.nTris;
         for (uint32_t i = tid; i < 16 * a.nNodes; i += 256) lo[i] = a.octNodes[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
+        for (uint32_t i = tid; i < 3 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
         __syncthreads();
-        return SceneView{nullptr, lt, nullptr, lo};
+        return SceneView{nullptr, lt, nullptr, lo, ls, lm};
     }
-    return SceneView{a.packedNodes, a.packedTris, a.skips, nullptr};
+    return SceneView{a.packedNodes, a.packedTris, a.skips, nullptr, a.shadeTris, a.shadeMats};
 }
 
-// LDS floats of the scene (the pool schedule's per-wave pools follow it)
-__device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) { return 16u * a.nNodes + 3u * a.nTris; }
+// LDS float4s of the scene (the pool schedule's per-wave pools follow it)
+__device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
+    return 16u * a.nNodes + 6u * a.nTris + 3u * a.nMats;
+}
 
 struct Traversal {
     float t;
@@ -329,22 +337,23 @@ struct LaneStats {
 // out of the loop (miss, or pdf <= 0 / NaN).
 template <class M, bool kStats>
 __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& radiance, F3& beta,
-                                             uint32_t& seed, const rt_cl_triangle* __restrict__ tris_full,
-                                             const rt_cl_material* __restrict__ mats, const KernelArgs& a,
+                                             uint32_t& seed, const SceneView& sc, const KernelArgs& a,
                                              LaneStats& st) {
     if (h.prim < 0) {
         radiance = radiance + beta * f3s(0.5f * a.skyboxIntensity);
         return false;
     }
     if (kStats) ++st.hits;
-    // hit record of the last accepted triangle (kernel_bvh.cl:142-147)
-    const rt_cl_triangle& tri = tris_full[h.prim];
+    // hit record of the last accepted triangle (kernel_bvh.cl:142-147), from the packed
+    // shading records (bit copies of the normals, mtlIndex and material fields)
+    const float4 s1 = sc.stris[3 * h.prim], s2 = sc.stris[3 * h.prim + 1], s3 = sc.stris[3 * h.prim + 2];
     const float w = (1.0f - h.u) - h.v;
-    const F3 normal = normalize<M>((load3(tri.v2.normal) * h.u + load3(tri.v3.normal) * h.v) +
-                                   load3(tri.v1.normal) * w);
+    const F3 normal = normalize<M>((F3{s2.x, s2.y, s2.z} * h.u + F3{s3.x, s3.y, s3.z} * h.v) +
+                                   F3{s1.x, s1.y, s1.z} * w);
     const F3 pos = ray.o + ray.d * h.t;
-    const rt_cl_material& mm = mats[tri.mtlIndex];
-    MatView m{load3(mm.diffuse), load3(mm.specular), load3(mm.emission), mm.roughness};
+    const uint32_t mi = 3u * __float_as_uint(s1.w);
+    const float4 m0 = sc.smats[mi], m1 = sc.smats[mi + 1], m2 = sc.smats[mi + 2];
+    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m0.w};
 
     radiance = radiance + (beta * m.emission) * 50.0f;
     F3 wi = f3s(0.0f);
@@ -361,8 +370,7 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
 
 // kernel_bvh.cl:349-384 (Render)
 template <class M, bool kOct, bool kStats>
-__device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* __restrict__ tris_full,
-                                     const rt_cl_material* __restrict__ mats, Ray ray,
+__device__ __forceinline__ F3 render(const SceneView& sc, Ray ray,
                                      uint32_t& seed, const KernelArgs& a,
                                      int32_t& prim_id, float& prim_t, LaneStats& st) {
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
@@ -374,7 +382,7 @@ __device__ __forceinline__ F3 render(const SceneView& sc, const rt_cl_triangle* 
             prim_id = h.prim;
             prim_t = h.t;
         }
-        if (!shade_bounce<M, kStats>(h, ray, radiance, beta, seed, tris_full, mats, a, st)) break;
+        if (!shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st)) break;
     }
     return F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
 }
@@ -452,7 +460,7 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
         const Ray ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
         int32_t pid = -1;
         float pt = 0.0f;
-        const F3 rad = render<M, kLdsScene, kStats>(sc, a.trisFull, a.materials, ray, seed, a, pid, pt, st);
+        const F3 rad = render<M, kLdsScene, kStats>(sc, ray, seed, a, pid, pt, st);
         finish_pixel<M>(a, gid, rad, pid, pt);
     }
     if (kStats) flush_stats(a, st, lane);
@@ -546,7 +554,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
                 pid = h.prim;
                 pt = h.t;
             }
-            bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, a.trisFull, a.materials, a, st);
+            bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
             ++bounce;
             if (!more || bounce >= bounces) {
                 const F3 rad{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
@@ -755,7 +763,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 pid = h.prim;
                 pt = h.t;
             }
-            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, a.trisFull, a.materials, a, st);
+            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
             ++bounce;
             if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
@@ -1104,8 +1112,7 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                 a.hitT[sp.gid] = sh.t;
             }
             LaneStats sst;
-            const bool more = shade_bounce<M, kStats>(sh, sr, sp.radiance, sp.beta, sp.seed, a.trisFull,
-                                                      a.materials, a, sst);
+            const bool more = shade_bounce<M, kStats>(sh, sr, sp.radiance, sp.beta, sp.seed, sc, a, sst);
             if (kStats && mine) st.hits += sst.hits;
             ++sp.bounce;
             const bool cont = mine && more && sp.bounce < bounces;
@@ -1233,6 +1240,24 @@ __global__ void pack_nodes(const rt_cl_bvh_node* __restrict__ in, float4* __rest
                                  __uint_as_float(meta));
 }
 
+__global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rt_cl_triangle& t = in[i];
+    out[3 * i] = make_float4(t.v1.normal.x, t.v1.normal.y, t.v1.normal.z, __uint_as_float(t.mtlIndex));
+    out[3 * i + 1] = make_float4(t.v2.normal.x, t.v2.normal.y, t.v2.normal.z, 0.0f);
+    out[3 * i + 2] = make_float4(t.v3.normal.x, t.v3.normal.y, t.v3.normal.z, 0.0f);
+}
+
+__global__ void pack_mats(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rt_cl_material& m = in[i];
+    out[3 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, m.roughness);
+    out[3 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, 0.0f);
+    out[3 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, 0.0f);
+}
+
 __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1288,9 +1313,12 @@ int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t sme
 }
 
 hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
-                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, hipStream_t st) {
+                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
+                       const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
     if (n_nodes) hipLaunchKernelGGL(pack_nodes, dim3((n_nodes + 255) / 256), dim3(256), 0, st, nodes, pn, n_nodes);
     if (n_tris) hipLaunchKernelGGL(pack_tris, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, pt, n_tris);
+    if (n_tris) hipLaunchKernelGGL(pack_shade, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, ps, n_tris);
+    if (n_mats) hipLaunchKernelGGL(pack_mats, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);
     return hipGetLastError();
 }
 

@@ -18,7 +18,9 @@ struct KernelArgs {
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
     const uint32_t* skips;              // derived from slot 2: [node][octant] DFS skip pointers
     const float4* octNodes;             // derived from slot 2: [node][octant] resolved records (LDS path)
-    uint32_t nNodes, nTris;
+    const float4* shadeTris;            // derived from slot 1: {n1, mtlIndex}, {n2}, {n3} per triangle
+    const float4* shadeMats;            // derived from slot 3: {diffuse, roughness}, {specular}, {emission}
+    uint32_t nNodes, nTris, nMats;
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)
     int32_t lightBounces, lightType;    // slots 8, 9
@@ -50,6 +52,7 @@ hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool ld
                                size_t smem, hipStream_t st);
 int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
 hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
-                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, hipStream_t st);
+                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
+                       const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk
