@@ -168,7 +168,8 @@ void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& sk
     }
 }
 
-// Octant-resolved node records for LDS-resident scenes: for node n and ray octant o,
+// Octant-resolved node records for LDS-resident scenes (stored as 16 planes of float4:
+// A[octant][node], then B[octant][node]): for node n and ray octant o,
 //   A = {near.x, near.y, near.z, far.x}, B = {far.y, far.z, hit_next, miss_next}
 // where near/far are the slab planes kernel_bvh.cl:156-169 selects by the ray's signs
 // (bit-exact copies of pmin/pmax), miss_next = skip[n][o] and hit_next is the near child
@@ -200,21 +201,25 @@ bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
         const float lo[3] = {x.bounds.pmin.x, x.bounds.pmin.y, x.bounds.pmin.z};
         const float hi[3] = {x.bounds.pmax.x, x.bounds.pmax.y, x.bounds.pmax.z};
         for (uint32_t o = 0; o < 8; ++o) {
-            uint32_t* r = &out[((size_t)i * 8 + o) * 8];
+            // octant-major planes A[o][node], B[o][node] (16 B each): lanes visiting different
+            // nodes in the same octant hit different LDS banks
+            uint32_t* ra = &out[((size_t)o * n + i) * 4];
+            uint32_t* rb = &out[((size_t)(8 + o) * n + i) * 4];
+            uint32_t* r[8] = {ra, ra + 1, ra + 2, ra + 3, rb, rb + 1, rb + 2, rb + 3};
             float nr[3], fr[3];
             for (int ax = 0; ax < 3; ++ax) {
                 const bool neg = (o >> ax) & 1u;
                 nr[ax] = neg ? hi[ax] : lo[ax];
                 fr[ax] = neg ? lo[ax] : hi[ax];
             }
-            r[0] = bits(nr[0]);
-            r[1] = bits(nr[1]);
-            r[2] = bits(nr[2]);
-            r[3] = bits(fr[0]);
-            r[4] = bits(fr[1]);
-            r[5] = bits(fr[2]);
-            r[6] = x.nPrimitives > 0 ? leaf : (((o >> x.axis) & 1u) ? x.offset : i + 1);
-            r[7] = skips[(size_t)i * 8 + o];
+            *r[0] = bits(nr[0]);
+            *r[1] = bits(nr[1]);
+            *r[2] = bits(nr[2]);
+            *r[3] = bits(fr[0]);
+            *r[4] = bits(fr[1]);
+            *r[5] = bits(fr[2]);
+            *r[6] = x.nPrimitives > 0 ? leaf : (((o >> x.axis) & 1u) ? x.offset : i + 1);
+            *r[7] = skips[(size_t)i * 8 + o];
         }
     }
     return ok;
@@ -590,7 +595,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     // (48 B per triangle, 48 B per material); no stack
     const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 48;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
-    const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0);
+    const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
+                        (k->sched == RT_SCHED_STEP ? 4 * rtk::kFinishWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;

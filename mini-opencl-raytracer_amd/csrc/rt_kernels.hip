@@ -91,8 +91,8 @@ __device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, 
 // ---- scene access ------------------------------------------------------------------------
 // Global (HBM/L2) scenes: packed node q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y,
 // bmax.z, offset, meta), meta = nPrimitives | axis << 16, plus [node][octant] skip pointers.
-// LDS scenes: octant-resolved records [node][octant] = {near.xyz, far.x}, {far.yz, hit_next,
-// miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
+// LDS scenes: octant-resolved records A[octant][node] = {near.xyz, far.x}, B[octant][node] =
+// {far.yz, hit_next, miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
 struct SceneView {
     const float4* nodes;    // global path
     const float4* tris;     // LDS or global
@@ -161,8 +161,8 @@ template <bool kOct>
 __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
                                            float t, uint32_t& next, uint32_t& first, uint32_t& count) {
     if (kOct) {
-        const uint32_t i = 2u * (8u * cur + r.sgn);
-        const float4 A = sc.onodes[i], B = sc.onodes[i + 1];
+        const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
+        const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
         float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
         float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
         t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
@@ -276,7 +276,11 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
         alpha = 2.0f / M::pow2(m.roughness) - 2.0f;
         (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
         const float r = next_rand(seed);
+#ifdef RT_EXP_NO_BRDF_POW
+        c = r * (1.0f / (alpha + 1.0f));  // timing experiment only (not the reference)
+#else
         c = M::pow(r, 1.0f / (alpha + 1.0f));  // cosTheta
+#endif
         sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - c * c));
     } else {
         const float s2 = next_rand(seed);
@@ -285,8 +289,13 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     }
     F3 s, t;
     onb<M>(n, s, t);
+#ifdef RT_EXP_NO_TRIG
+    const F3 pa = (s * (1.0f - phi)) * sinT;  // timing experiment only (not the reference)
+    const F3 pb = (t * phi) * sinT;
+#else
     const F3 pa = (s * M::cos(phi)) * sinT;
     const F3 pb = (t * M::sin(phi)) * sinT;
+#endif
     const F3 dir = normalize<M>((pa + pb) + n * c);
     if (spec) {
         const F3 wh = dir;
@@ -396,9 +405,15 @@ __device__ __forceinline__ void finish_color(const KernelArgs& a, uint32_t gid, 
     } else {
         const float4 old = a.result[gid];
         const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
+#ifdef RT_EXP_NO_GAMMA
+        const F3 lin{old.x * old.x, old.y * old.y, old.z * old.z};  // timing experiment only
+        const F3 acc = ((lin * fm1) + rad) / fc;
+        out = acc;
+#else
         const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
         const F3 acc = ((lin * fm1) + rad) / fc;
         out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+#endif
     }
     a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
 }
@@ -580,6 +595,25 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
 // at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Finish queue: the gamma accumulation (kernel_bvh.cl:449-455, six pow per pixel) of
+// finished paths runs 64 pixels at a time instead of with the few lanes whose paths
+// happen to end in a refill round.  Pixels are independent and each is written once per
+// launch, so the order of finishing does not matter.
+constexpr uint32_t kFinishSlots = 64;
+static_assert(kFinishWaveBytes == kFinishSlots * 16, "finish queue layout");
+
+template <class M>
+__device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4* fq, uint32_t n, uint32_t lane) {
+    if (lane < n) {
+        const float4 e = fq[lane];
+        finish_color<M>(a, __float_as_uint(e.w), F3{e.x, e.y, e.z});
+    }
+}
 // steps of the chosen kind per scheduling decision (thresholds are re-checked after each
 // burst): the per-step ballots and threshold tests cost about as much as a node visit
 #ifndef RT_NODE_BURST
@@ -607,6 +641,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int lane = tid & 63;
     const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
     const uint32_t kShadeMin = a.shadeMin;    // shade when this many lanes are ready
+
+    // per-wave finish queue in LDS (after the scene): {radiance, gid} of finished paths
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    float4* fq = smem + (kLdsScene ? lds_scene_f4(a) : 0u) + (uint32_t)(tid >> 6) * kFinishSlots;
+    uint32_t fq_n = 0;  // wave-uniform
 
     LaneStats st;
     uint32_t state = kIdle;
@@ -636,9 +675,28 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 ++u_rrounds;
                 u_rlanes += n_free;
             }
-            if (state == kDone) {
-                finish_pixel<M>(a, gid, radiance, pid, pt);
-                state = kIdle;
+            // finished paths: hit outputs now, the gamma accumulation through the finish queue
+            const unsigned long long done = __ballot(state == kDone);
+            if (done != 0ull) {
+                const uint32_t nd = (uint32_t)__popcll(done);
+                const uint32_t rank = lane_rank(done);
+                const uint32_t fit = kFinishSlots - fq_n;
+                if (state == kDone) {
+                    if (a.hitIds) {
+                        a.hitIds[gid] = pid;
+                        a.hitT[gid] = pt;
+                    }
+                    if (rank < fit) fq[fq_n + rank] = make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(gid));
+                }
+                if (nd >= fit) {
+                    finish_queued<M>(a, fq, kFinishSlots, lane);
+                    if (state == kDone && rank >= fit)
+                        fq[rank - fit] = make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(gid));
+                    fq_n = nd - fit;
+                } else {
+                    fq_n += nd;
+                }
+                if (state == kDone) state = kIdle;
             }
             while (!exhausted) {
                 const unsigned long long idle = __ballot(state == kIdle);
@@ -777,6 +835,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         }
         if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tC;
     }
+    finish_queued<M>(a, fq, fq_n, lane);
     if (kStats) {
         flush_stats(a, st, lane);
         if (lane == 0) {
@@ -926,10 +985,6 @@ __device__ __forceinline__ void pool_get_lane(const PoolView& p, uint32_t s, uin
     state = __float_as_uint(c4.x);
     ps = PathState{__float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w), F3{c5.x, c5.y, c5.z},
                    F3{c5.w, c6.x, c6.y}};
-}
-
-__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 template <class M, bool kLdsScene, bool kStats>
