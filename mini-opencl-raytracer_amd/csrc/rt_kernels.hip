@@ -195,13 +195,16 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
 }
 
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
-// early returns (det, u, v) become one accept predicate.  The values computed are the
+// early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
 // ones the reference computes where it reaches them; the rest are discarded.  A wave
 // tests ~25 lanes' triangles at once and nearly always has some lane past every early
 // return, so the branches saved no arithmetic and cost exec-mask bookkeeping.
+struct TriEval {
+    float det, u, v, t;
+};
+
 template <class M>
-__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
-                                             Traversal& h) {
+__device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
     const float4 a = tri[0], b = tri[1], c = tri[2];
     const F3 p1{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
     const F3 pvec = M::cross(r.d, e2);
@@ -212,14 +215,33 @@ __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, con
     const F3 qvec = M::cross(tvec, e1);
     const float v = M::dot(r.d, qvec) * inv_det;
     const float t = M::dot(e2, qvec) * inv_det;
+    return TriEval{det, u, v, t};
+}
+
+// kUV = false: keep only {t, primitive} during the walk (two fewer live registers); the
+// barycentrics of the closest hit are re-evaluated at shading time (hit_uv) from the same
+// triangle and ray, which reproduces the accepted values bit for bit.
+template <class M, bool kUV = true>
+__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
+                                             Traversal& h) {
+    const TriEval e = tri_eval<M>(tri, r);
     // (det < 1e-8 || -det > 1e-8) == det < 1e-8 (NaN falls through, as in the reference)
-    const bool ok = !(det < kHitEps) & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) & !(u + v > 1.0f) & (t < h.t);
+    const bool ok = !(e.det < kHitEps) & !(e.u < 0.0f) & !(e.u > 1.0f) & !(e.v < 0.0f) &
+                    !(e.u + e.v > 1.0f) & (e.t < h.t);
     if (ok) {
-        h.t = t;
+        h.t = e.t;
         h.prim = idx;
-        h.u = u;
-        h.v = v;
+        if (kUV) {
+            h.u = e.u;
+            h.v = e.v;
+        }
     }
+}
+
+template <class M>
+__device__ __forceinline__ Traversal with_uv(const SceneView& sc, const Traversal& h, const Ray& r) {
+    const TriEval e = tri_eval<M>(sc.tris + 3 * (size_t)(h.prim < 0 ? 0 : h.prim), r);
+    return Traversal{h.t, h.prim, e.u, e.v};
 }
 
 // kernel_bvh.cl:171-219 (Intersect), replayed with the per-octant skip pointers: visiting
@@ -650,8 +672,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     LaneStats st;
     uint32_t state = kIdle;
     uint32_t gid = 0, seed = 0, bounce = 0;
-    int32_t pid = -1;
-    float pt = 0.0f;
     Ray ray{};
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
@@ -682,10 +702,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 const uint32_t rank = lane_rank(done);
                 const uint32_t fit = kFinishSlots - fq_n;
                 if (state == kDone) {
-                    if (a.hitIds) {
-                        a.hitIds[gid] = pid;
-                        a.hitT[gid] = pt;
-                    }
                     if (rank < fit) fq[fq_n + rank] = make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(gid));
                 }
                 if (nd >= fit) {
@@ -729,8 +745,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         radiance = f3s(0.0f);
                         beta = f3s(1.0f);
                         bounce = 0;
-                        pid = -1;
-                        pt = 0.0f;
                         if (bounces > 0u) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
@@ -738,6 +752,10 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             if (kStats) ++st.rays;
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
+                            if (a.hitIds) {
+                                a.hitIds[gid] = -1;
+                                a.hitT[gid] = 0.0f;
+                            }
                         }
                     }
                 }
@@ -798,7 +816,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 for (int rep = 0; rep < RT_TRI_BURST; ++rep) {
                     if (state == kLeaf) {
                         if (kStats) ++st.tests;
-                        ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                        ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
                         ++leaf_i;
                         if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
                     }
@@ -817,11 +835,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
         }
         if (state == kShade) {
-            if (bounce == 0u) {
-                pid = h.prim;
-                pt = h.t;
+            if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension)
+                a.hitIds[gid] = h.prim;
+                a.hitT[gid] = h.t;
             }
-            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
+            const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, h, ray), ray, radiance, beta, seed, sc, a, st);
             ++bounce;
             if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
