@@ -51,6 +51,12 @@ for step in "$@"; do
                 for v in mini-opencl-raytracer_amd/lib/variants/*.so; do n=$(basename $v .so); \
                   RT_HIP_LIB=$v run ab_${n}_$m 300 python bench.py --math $m --no-cpu-baseline --steps 3 || exit $?; done; \
                 run ab_main_$m 300 python bench.py --math $m --no-cpu-baseline --steps 3 || exit $?; done ;;
+    configs) run cfg3_default 600 python bench.py && \
+             run cfg3_pinned 300 python bench.py --math pinned --no-cpu-baseline && \
+             run cfg2_1080p 300 python bench.py --width 1920 --height 1080 --bounces 2 --frames 1 --steps 20 --no-cpu-baseline && \
+             run cfg1_512 300 python bench.py --width 512 --height 512 --bounces 1 --frames 1 --steps 50 --no-cpu-baseline && \
+             run cfg5_bunny 300 python bench.py --scene bunny --no-cpu-baseline && \
+             run cfg5_bunny_pinned 300 python bench.py --scene bunny --math pinned --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done
