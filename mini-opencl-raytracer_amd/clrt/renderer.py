@@ -99,6 +99,13 @@ class Raytracer:
         """Last read-back frame as (H, W, 3); row 0 is the bottom row (GL order)."""
         return self.pixels.reshape(self.height, self.width, 4)[:, :, :3]
 
+    def save(self, path: str) -> None:
+        """Write the last read-back frame (.png, else binary .ppm) -- the display step the
+        reference does with glTexSubImage2D (CLRaytracer.cpp:64-67)."""
+        from . import image
+        w = image.write_png if path.lower().endswith(".png") else image.write_ppm
+        w(path, self.pixels, self.width, self.height)
+
     def release(self) -> None:
         for b in self._scene_bufs:
             b.release()

@@ -4,11 +4,11 @@
 // (CLRaytracer.cpp:12-148) through the reference-shaped C++ wrapper: Init (context +
 // kernel + output buffer), CLOBJloader::Load + CreateBVHTrees + SetupBuffers, then
 // RenderFrame per frame (uniforms, ExecuteKernel(W*H), ReadBuffer, Finish,
-// ++m_FrameCount).  The GL blit is replaced by a PPM writer (rows flipped: row 0 of the
+// ++m_FrameCount).  The GL blit is replaced by the image writer (rt_image.h; rows flipped: row 0 of the
 // output is the bottom of the image, as glTexSubImage2D shows it).
 //
 // usage: rt_render [obj=path] [w=W] [h=H] [frames=N] [bounces=B] [light=T] [sky=S]
-//                  [out=file.ppm] [device=D] [math=pinned|devicelib]
+//                  [out=file.ppm|file.png] [device=D] [math=pinned|devicelib]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/rt_cl_compat.hpp"
+#include "../../include/rt_image.h"
 #include "../../include/rt_scene.h"
 
 using rtcl::RenderKernelArgument_t;
@@ -32,24 +33,6 @@ std::string arg(int argc, char** argv, const char* key, const char* dflt) {
     for (int i = 1; i < argc; ++i)
         if (std::strncmp(argv[i], key, n) == 0 && argv[i][n] == '=') return argv[i] + n + 1;
     return dflt;
-}
-
-void write_ppm(const char* path, const std::vector<float>& px, unsigned W, unsigned H) {
-    FILE* f = std::fopen(path, "wb");
-    if (!f) return;
-    std::fprintf(f, "P6\n%u %u\n255\n", W, H);
-    std::vector<unsigned char> row(3 * (size_t)W);
-    for (unsigned y = 0; y < H; ++y) {
-        const unsigned src = H - 1 - y;
-        for (unsigned x = 0; x < W; ++x)
-            for (int c = 0; c < 3; ++c) {
-                float v = px[4 * ((size_t)src * W + x) + c];
-                v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-                row[3 * x + c] = (unsigned char)(v * 255.0f + 0.5f);
-            }
-        std::fwrite(row.data(), 1, row.size(), f);
-    }
-    std::fclose(f);
 }
 
 }  // namespace
@@ -122,7 +105,9 @@ int main(int argc, char** argv) {
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         std::printf("rendered %d frame(s) %ux%u, %d bounces: %.3f ms/frame (incl. readback)\n", frames, W, H,
                     lightBounces, ms / (frames > 0 ? frames : 1));
-        write_ppm(out.c_str(), pixels, W, H);
+        const bool png = out.size() > 4 && out.compare(out.size() - 4, 4, ".png") == 0;
+        const int wrc = png ? rtiWritePNG(out.c_str(), pixels.data(), W, H) : rtiWritePPM(out.c_str(), pixels.data(), W, H);
+        if (wrc) std::fprintf(stderr, "writing %s failed: %d\n", out.c_str(), wrc);
     } catch (const rtcl::CLException& ex) {
         std::fprintf(stderr, "Caught exception: %s\n", ex.what());
         return 1;

@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared(header):
     txt = open(os.path.join(REPO, "include", header)).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return set(re.findall(r"\b(rts?[A-Z]\w+)\s*\(", txt)) - {"rtGetErrorString"}
+    return set(re.findall(r"\b(rt[si]?[A-Z]\w+)\s*\(", txt)) - {"rtGetErrorString"}
 
 
 def test_hip_library_exports_header_symbols():
@@ -33,6 +33,15 @@ def test_scene_library_exports_header_symbols():
     for name in names:
         assert hasattr(lib, name), name
     assert set(N.SCENE_EXPORTS) == names
+
+
+def test_image_writer_exports_header_symbols():
+    from clrt import image
+    lib = ctypes.CDLL(clrt.SCENE_LIB_PATH)
+    names = _declared("rt_image.h")
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(image.IMAGE_EXPORTS) == names
 
 
 def test_build_info_without_gpu():
