@@ -645,6 +645,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #define RT_TRI_BURST 2
 #endif
 
+
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
 template <class M, bool kLdsScene, bool kStats>
