@@ -93,6 +93,9 @@ struct rt_kernel_s {
     float4* shade_mats = nullptr;      // compact materials
     size_t shade_tris_cap = 0, shade_mats_cap = 0;
     bool oct_ok = false;               // every leaf fits the records' inline {first, count}
+    float4* g_nodes = nullptr;         // global-scene node records (64 B, top of the tree first)
+    size_t g_nodes_cap = 0;
+    uint32_t n_top = 0, top_limit = 256;  // nodes of g_nodes staged in LDS (global path)
     size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
@@ -237,6 +240,61 @@ int ensure_dev(T*& p, size_t& cap, size_t count) {
     return RT_SUCCESS;
 }
 
+// Node records for scenes read from HBM/L2 (64 B = half a cache line, so one visit touches
+// one line): q0 = {bmin.xyz, bmax.x}, q1 = {bmax.yz, c0, c1}, q2/q3 = skip[8].  Interior:
+// c0 = first child, c1 = second child | axis << 30; leaf: c0 = first triangle,
+// c1 = count | 3 << 30.  Children and skips are explicit, so the nodes can be renumbered:
+// the first `top` nodes in breadth-first order (the top of the tree, visited by nearly every
+// ray) come first and are staged in LDS; the rest keep their depth-first order.  The walk is
+// the same tree and skip table, so visits, tests and results are unchanged.
+void build_global_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
+                        uint32_t top, std::vector<uint32_t>& out, uint32_t* n_top) {
+    std::vector<uint32_t> order, newid(n, 0xffffffffu);
+    order.reserve(n);
+    std::vector<uint32_t> q = {0};
+    for (size_t h = 0; h < q.size() && order.size() < top; ++h) {
+        const uint32_t i = q[h];
+        newid[i] = (uint32_t)order.size();
+        order.push_back(i);
+        if (nd[i].nPrimitives == 0) {
+            q.push_back(i + 1);
+            q.push_back(nd[i].offset);
+        }
+    }
+    *n_top = (uint32_t)order.size();
+    for (uint32_t i = 0; i < n; ++i)
+        if (newid[i] == 0xffffffffu) {
+            newid[i] = (uint32_t)order.size();
+            order.push_back(i);
+        }
+    auto map = [&](uint32_t x) { return x == 0xffffffffu ? x : newid[x]; };
+    auto bits = [](float f) {
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        return u;
+    };
+    out.assign((size_t)n * 16, 0u);
+    for (uint32_t p = 0; p < n; ++p) {
+        const uint32_t i = order[p];
+        const rt_cl_bvh_node& x = nd[i];
+        uint32_t* r = &out[(size_t)p * 16];
+        r[0] = bits(x.bounds.pmin.x);
+        r[1] = bits(x.bounds.pmin.y);
+        r[2] = bits(x.bounds.pmin.z);
+        r[3] = bits(x.bounds.pmax.x);
+        r[4] = bits(x.bounds.pmax.y);
+        r[5] = bits(x.bounds.pmax.z);
+        if (x.nPrimitives > 0) {
+            r[6] = x.offset;
+            r[7] = (uint32_t)x.nPrimitives | (3u << 30);
+        } else {
+            r[6] = map(i + 1);
+            r[7] = map(x.offset) | ((uint32_t)x.axis << 30);
+        }
+        for (int o = 0; o < 8; ++o) r[8 + o] = map(skips[(size_t)i * 8 + o]);
+    }
+}
+
 int prepare_scene(rt_kernel k) {
     rt_mem tm = k->bufs[RT_ARG_BUFFER_SCENE], nm = k->bufs[RT_ARG_BUFFER_NODE],
            mm = k->bufs[RT_ARG_BUFFER_MATERIAL];
@@ -282,6 +340,17 @@ int prepare_scene(rt_kernel k) {
         if (e != hipSuccess) return map_hip(e);
         k->packed_skips_cap = nn;
     }
+    if (nn >= (1u << 30)) return RT_INVALID_MEM_OBJECT;  // node indices share a word with the axis
+    std::vector<uint32_t> gn;
+    uint32_t n_top = 0;
+    build_global_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, k->top_limit, gn, &n_top);
+    rc = ensure_dev(k->g_nodes, k->g_nodes_cap, (size_t)nn * 4);
+    if (rc) return rc;
+    {
+        hipError_t e = hipMemcpyAsync(k->g_nodes, gn.data(), gn.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                      k->ctx->stream);
+        if (e != hipSuccess) return map_hip(e);
+    }
     std::vector<uint32_t> oct;
     const bool oct_ok = build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct);
     rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)nn * 16);
@@ -317,6 +386,7 @@ int prepare_scene(rt_kernel k) {
     k->n_mats = nmat;
     k->depth = depth;
     k->oct_ok = oct_ok;
+    k->n_top = n_top;
     k->packed_for_tris = tm;
     k->packed_tris_gen = tm->generation;
     k->packed_for_nodes = nm;
@@ -453,6 +523,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
+    if (const char* v = std::getenv("RT_TOP_NODES")) k->top_limit = (uint32_t)std::max(0, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RT_POOL_SHADE")) k->pool_shade = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_PARK_MIN")) k->park_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_LOW_WORK")) k->low_work = (uint32_t)std::max(1, std::min(128, std::atoi(v)));
@@ -486,6 +557,7 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->packed_skips) (void)hipFree(k->packed_skips);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
+    if (k->g_nodes) (void)hipFree(k->g_nodes);
     if (k->shade_tris) (void)hipFree(k->shade_tris);
     if (k->shade_mats) (void)hipFree(k->shade_mats);
     if (k->dstats) (void)hipFree(k->dstats);
@@ -545,6 +617,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.packedTris = k->packed_tris;
     a.skips = k->packed_skips;
     a.octNodes = k->oct_nodes;
+    a.gNodes = k->g_nodes;
     a.shadeTris = k->shade_tris;
     a.shadeMats = k->shade_mats;
     a.nMats = k->n_mats;
@@ -595,7 +668,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     // (48 B per triangle, 48 B per material); no stack
     const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 48;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
-    const size_t smem = (lds ? scene_bytes : 0) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
+    a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
+    const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
                         (k->sched == RT_SCHED_STEP ? 4 * rtk::kFinishWaveBytes : 0);
     k->last_lds = lds;
 

@@ -94,7 +94,7 @@ __device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, 
 // LDS scenes: octant-resolved records A[octant][node] = {near.xyz, far.x}, B[octant][node] =
 // {far.yz, hit_next, miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
 struct SceneView {
-    const float4* nodes;    // global path
+    const float4* nodes;    // global path: 64-B records (generic pointer: the top in LDS)
     const float4* tris;     // LDS or global
     const uint32_t* skips;  // global path: [node][octant] next node in the octant's DFS order
     const float4* onodes;   // LDS path: octant-resolved node records
@@ -122,12 +122,17 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
         __syncthreads();
         return SceneView{nullptr, lt, nullptr, lo, ls, lm};
     }
-    return SceneView{a.packedNodes, a.packedTris, a.skips, nullptr, a.shadeTris, a.shadeMats};
+    // global scene: the top-of-tree node records into LDS, the rest read from HBM/L2
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < 4 * a.nTop; i += 256) smem[i] = a.gNodes[i];
+    __syncthreads();
+    return SceneView{a.gNodes, a.packedTris, nullptr, smem, a.shadeTris, a.shadeMats};
 }
 
-// LDS float4s of the scene (the pool schedule's per-wave pools follow it)
+// LDS float4s of the scene (the finish queue / pool follow it)
+template <bool kLdsScene>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return 16u * a.nNodes + 6u * a.nTris + 3u * a.nMats;
+    return kLdsScene ? 16u * a.nNodes + 6u * a.nTris + 3u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -177,19 +182,21 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
         count = ((hn >> 24) & 0x3fu) + 1u;
         return leaf;
     }
-    const float4 q0 = sc.nodes[2 * cur];
-    const float4 q1 = sc.nodes[2 * cur + 1];
-    next = sc.skips[8 * cur + r.sgn];
+    // global 64-B record; the first nTop records are read from their LDS copy (one flat load
+    // serves both address spaces)
+    const float4* nd = (cur < a.nTop ? sc.onodes : sc.nodes) + 4u * cur;
+    const float4 q0 = nd[0];
+    const float4 q1 = nd[1];
+    next = reinterpret_cast<const uint32_t*>(nd + 2)[r.sgn];
     if (ray_bounds(q0, q1, r, t)) {
-        const uint32_t off = __float_as_uint(q1.z);
-        const uint32_t meta = __float_as_uint(q1.w);
-        const uint32_t np = meta & 0xffffu;
-        if (np > 0) {
-            first = off;
-            count = np;
+        const uint32_t c0 = __float_as_uint(q1.z), c1 = __float_as_uint(q1.w);
+        const uint32_t axis = c1 >> 30;
+        if (axis == 3u) {
+            first = c0;
+            count = c1 & 0x3fffffffu;
             return true;
         }
-        next = ((r.sgn >> (meta >> 16)) & 1u) ? off : cur + 1;
+        next = ((r.sgn >> axis) & 1u) ? (c1 & 0x3fffffffu) : c0;
     }
     return false;
 }
@@ -667,7 +674,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 
     // per-wave finish queue in LDS (after the scene): {radiance, gid} of finished paths
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    float4* fq = smem + (kLdsScene ? lds_scene_f4(a) : 0u) + (uint32_t)(tid >> 6) * kFinishSlots;
+    float4* fq = smem + lds_scene_f4<kLdsScene>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
     uint32_t fq_n = 0;  // wave-uniform
 
     LaneStats st;
@@ -1011,7 +1018,7 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const int tid = threadIdx.x;
     const SceneView sc = stage_scene<kLdsScene>(a);
-    const uint32_t scene_f4 = kLdsScene ? lds_scene_f4(a) : 0u;
+    const uint32_t scene_f4 = lds_scene_f4<kLdsScene>(a);
     float4* region = smem + scene_f4 + (uint32_t)(tid >> 6) * (kPoolWaveBytes / 16u);
     uint32_t* stacks = reinterpret_cast<uint32_t*>(region + kPoolChunks * kPoolSlots);
     const PoolView pv{region, stacks, stacks + kPoolSlots, stacks + 2 * kPoolSlots};

@@ -40,6 +40,11 @@ for step in "$@"; do
     dist2) run dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --math devicelib ;;
     benchbunny) run bench_bunny 600 python bench.py --scene bunny --no-cpu-baseline --steps 3 ;;
     phase) run phase 300 python scripts/phase_profile.py ;;
+    phasebunny) RT_PHASE_SCENE=bunny run phase_bunny 300 python scripts/phase_profile.py ;;
+    pmcbunny) run pmcb_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcb_fetch -o run -- python bench.py --scene bunny --steps 1 --warmup 0 --no-cpu-baseline && \
+              run pmcb_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmcb_sq -o run -- python bench.py --scene bunny --steps 1 --warmup 0 --no-cpu-baseline && \
+              run pmcb_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmcb_sq2 -o run -- python bench.py --scene bunny --steps 1 --warmup 0 --no-cpu-baseline && \
+              python scripts/pmc_summary.py $OUT/pmcb_summary.json $OUT/pmcb_fetch $OUT/pmcb_sq $OUT/pmcb_sq2 > $OUT/pmcb_summary.txt ;;
     phasepool) run phase_pool 300 python scripts/phase_profile.py step pool ;;
     poolpar) run pool_parity 600 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "schedules or interleaved" ;;
     benchpool) run bench_pool_dl 600 python bench.py --sched pool --no-cpu-baseline && \

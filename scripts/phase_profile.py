@@ -11,7 +11,11 @@ import clrt  # noqa: E402
 from clrt import _native as N  # noqa: E402
 from hip_helpers import HipRenderer  # noqa: E402
 
-sc = clrt.scene.cornell()
+if os.environ.get("RT_PHASE_SCENE") == "bunny":
+    from clrt import proxy
+    sc = proxy.bunny_proxy()
+else:
+    sc = clrt.scene.cornell()
 scheds = sys.argv[1:] or ["step"]
 for name in scheds:
   sched = {"step": N.SCHED_STEP, "pool": N.SCHED_POOL}[name]
