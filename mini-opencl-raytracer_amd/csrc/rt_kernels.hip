@@ -651,6 +651,13 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
 #endif
+// the same for scenes read from HBM/L2 (global path)
+#ifndef RT_GNODE_BURST
+#define RT_GNODE_BURST RT_NODE_BURST
+#endif
+#ifndef RT_GTRI_BURST
+#define RT_GTRI_BURST RT_TRI_BURST
+#endif
 
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
@@ -804,9 +811,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     u_nlanes += n_trav;
                 }
             }
+            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
+            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
             if (!leaf_step) {
 #pragma unroll
-                for (int rep = 0; rep < RT_NODE_BURST; ++rep) {
+                for (int rep = 0; rep < kNodeBurst; ++rep) {
                     if (state == kTrav) {
                         if (kStats) ++st.visits;
                         uint32_t next, first = 0, count = 0;
@@ -821,7 +830,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 }
             } else {
 #pragma unroll
-                for (int rep = 0; rep < RT_TRI_BURST; ++rep) {
+                for (int rep = 0; rep < kTriBurst; ++rep) {
                     if (state == kLeaf) {
                         if (kStats) ++st.tests;
                         ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
