@@ -269,7 +269,9 @@ def main():
                  "generated bunny-class proxy OBJ (clrt/proxy.py)") + "; rays generated in-kernel",
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "schedule": args.sched, "parallelism": f"interleaved 8-row bands x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+                   "math": args.math, "schedule": args.sched, "parallelism": f"interleaved 8-row bands x{world}" + (
+                       (" + RCCL gather to rank 0" if args.dist_backend == "nccl" else " + gloo gather to rank 0 (host-staged)")
+                       if world > 1 else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
