@@ -48,6 +48,18 @@ int rtsGetMaterials(const rt_scene* s, const rt_cl_material** mats, size_t* coun
 int rtsGetTreeStats(const rt_scene* s, unsigned* max_depth, unsigned* n_leaves,
                     unsigned* max_leaf_prims);
 
+/* Wrap caller arrays that are already built (BVH order + flattened nodes), e.g. to cache a
+ * scene built elsewhere.  Node child / leaf ranges are validated. */
+int rtsFromArrays(const rt_cl_triangle* tris, size_t n_tris, const rt_cl_bvh_node* nodes, size_t n_nodes,
+                  const rt_cl_material* mats, size_t n_mats, unsigned max_prims_in_node, rt_scene** out);
+
+/* Binary scene cache: the three device arrays exactly as built, so a large
+ * OBJ is parsed and its BVH built once.  Format: "RTSCENE1", u32 version, u32
+ * maxPrimitivesInNode, u64 triangle / node / material counts, the raw arrays, u64 FNV-1a of
+ * everything before it.  A bad magic, size or checksum is RT_PARSE_ERROR. */
+int rtsSaveScene(const rt_scene* s, const char* path);
+int rtsLoadScene(const char* path, rt_scene** out);
+
 void rtsRelease(rt_scene* s);
 
 #ifdef __cplusplus

@@ -129,6 +129,10 @@ _SCENE_PROTOS = {
     "rtsGetMaterials": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
     "rtsGetTreeStats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
                                        ctypes.POINTER(ctypes.c_uint)]),
+    "rtsFromArrays": (ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
+                                     ctypes.c_uint, ctypes.POINTER(_vp)]),
+    "rtsSaveScene": (ctypes.c_int, [_vp, ctypes.c_char_p]),
+    "rtsLoadScene": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "rtsRelease": (None, [_vp]),
 }
 SCENE_EXPORTS = tuple(_SCENE_PROTOS)

@@ -19,7 +19,7 @@ import os
 
 import numpy as np
 
-from .scene import Scene, load_obj
+from .scene import Scene, load_obj, load_scene, save_scene
 
 _REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 GEN_DIR = os.path.join(_REPO, "scenes", "generated")
@@ -110,9 +110,16 @@ def write_bunny_proxy(obj_path: str, n_theta: int = 133, n_phi: int = 133) -> in
     return len(out)
 
 
-def bunny_proxy(max_prims_in_node: int = 4, path: str | None = None) -> Scene:
-    """Generate (if needed) and load the proxy through the product OBJ loader + SAH builder."""
+def bunny_proxy(max_prims_in_node: int = 4, path: str | None = None, cache: bool = True) -> Scene:
+    """Generate (if needed) and load the proxy through the product OBJ loader + SAH builder;
+    the built arrays are kept in a binary scene cache next to the OBJ (rtsSaveScene)."""
     path = path or os.path.join(GEN_DIR, "bunny_proxy.obj")
     if not os.path.exists(path):
         write_bunny_proxy(path)
-    return load_obj(path, max_prims_in_node)
+    cpath = f"{path[:-4]}.mp{max_prims_in_node}.rtscene"
+    if cache and os.path.exists(cpath) and os.path.getmtime(cpath) >= os.path.getmtime(path):
+        return load_scene(cpath, max_prims_in_node)
+    sc = load_obj(path, max_prims_in_node)
+    if cache:
+        save_scene(sc, cpath)
+    return sc

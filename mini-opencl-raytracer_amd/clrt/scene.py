@@ -92,6 +92,33 @@ def build_bvh(triangles: np.ndarray, materials: np.ndarray, max_prims_in_node: i
     return Scene(t, n, m, max_prims_in_node)
 
 
+def save_scene(scene: Scene, path: str) -> None:
+    """Binary scene cache (rtsSaveScene): the three arrays exactly as built."""
+    lib = scene_lib()
+    t = np.ascontiguousarray(scene.triangles, dtype=TRIANGLE_DTYPE)
+    n = np.ascontiguousarray(scene.nodes, dtype=NODE_DTYPE)
+    m = np.ascontiguousarray(scene.materials, dtype=MATERIAL_DTYPE)
+    h = ctypes.c_void_p()
+    check(lib.rtsFromArrays(t.ctypes.data, t.shape[0], n.ctypes.data, n.shape[0], m.ctypes.data, m.shape[0],
+                            int(scene.max_prims_in_node), ctypes.byref(h)), "rtsFromArrays")
+    try:
+        check(lib.rtsSaveScene(h, path.encode()), f"Failed to write scene cache {path}")
+    finally:
+        lib.rtsRelease(h)
+
+
+def load_scene(path: str, max_prims_in_node: int = 4) -> Scene:
+    """Read a binary scene cache written by save_scene / rtsSaveScene."""
+    lib = scene_lib()
+    h = ctypes.c_void_p()
+    check(lib.rtsLoadScene(path.encode(), ctypes.byref(h)), f"Failed to load scene cache {path}")
+    try:
+        tris, nodes, mats = _copy_out(lib, h)
+    finally:
+        lib.rtsRelease(h)
+    return Scene(tris, nodes, mats, max_prims_in_node)
+
+
 _REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CORNELL_NPZ = os.path.join(_REPO, "scenes", "cornell_scene.npz")
 

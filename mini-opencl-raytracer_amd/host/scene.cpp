@@ -466,6 +466,119 @@ int rtsGetTreeStats(const rt_scene* s, unsigned* max_depth, unsigned* n_leaves,
     return RT_SUCCESS;
 }
 
+namespace {
+
+constexpr char kSceneMagic[8] = {'R', 'T', 'S', 'C', 'E', 'N', 'E', '1'};
+constexpr uint32_t kSceneVersion = 1;
+
+uint64_t fnv1a(const void* p, size_t n, uint64_t h) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+int check_arrays(const std::vector<rt_cl_bvh_node>& nodes, size_t n_tris) {
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const rt_cl_bvh_node& x = nodes[i];
+        if (x.nPrimitives > 0) {
+            if ((uint64_t)x.offset + x.nPrimitives > n_tris) return RT_INVALID_VALUE;
+        } else if (x.offset <= i + 1 || x.offset >= nodes.size() || i + 1 >= nodes.size()) {
+            return RT_INVALID_VALUE;
+        }
+    }
+    return RT_SUCCESS;
+}
+
+}  // namespace
+
+int rtsFromArrays(const rt_cl_triangle* tris, size_t n_tris, const rt_cl_bvh_node* nodes, size_t n_nodes,
+                  const rt_cl_material* mats, size_t n_mats, unsigned max_prims_in_node, rt_scene** out) {
+    if (!out || (!tris && n_tris) || (!nodes && n_nodes) || (!mats && n_mats)) return RT_INVALID_VALUE;
+    *out = nullptr;
+    std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
+    if (!s) return RT_OUT_OF_HOST_MEMORY;
+    s->tris.assign(tris, tris + n_tris);
+    s->nodes.assign(nodes, nodes + n_nodes);
+    s->mats.assign(mats, mats + n_mats);
+    s->max_prims = max_prims_in_node;
+    int rc = check_arrays(s->nodes, s->tris.size());
+    if (rc) return rc;
+    *out = s.release();
+    return RT_SUCCESS;
+}
+
+int rtsSaveScene(const rt_scene* s, const char* path) {
+    if (!s || !path) return RT_INVALID_VALUE;
+    uint32_t hdr32[2] = {kSceneVersion, s->max_prims};
+    uint64_t hdr64[3] = {s->tris.size(), s->nodes.size(), s->mats.size()};
+    uint64_t h = 14695981039346656037ull;
+    h = fnv1a(kSceneMagic, 8, h);
+    h = fnv1a(hdr32, sizeof(hdr32), h);
+    h = fnv1a(hdr64, sizeof(hdr64), h);
+    h = fnv1a(s->tris.data(), s->tris.size() * sizeof(rt_cl_triangle), h);
+    h = fnv1a(s->nodes.data(), s->nodes.size() * sizeof(rt_cl_bvh_node), h);
+    h = fnv1a(s->mats.data(), s->mats.size() * sizeof(rt_cl_material), h);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return RT_INVALID_VALUE;
+    bool ok = std::fwrite(kSceneMagic, 1, 8, f) == 8 && std::fwrite(hdr32, sizeof(hdr32), 1, f) == 1 &&
+              std::fwrite(hdr64, sizeof(hdr64), 1, f) == 1;
+    ok = ok && std::fwrite(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size(), f) == s->tris.size();
+    ok = ok && std::fwrite(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size(), f) == s->nodes.size();
+    ok = ok && std::fwrite(s->mats.data(), sizeof(rt_cl_material), s->mats.size(), f) == s->mats.size();
+    ok = ok && std::fwrite(&h, sizeof(h), 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_SUCCESS : RT_OUT_OF_RESOURCES;
+}
+
+int rtsLoadScene(const char* path, rt_scene** out) {
+    if (!path || !out) return RT_INVALID_VALUE;
+    *out = nullptr;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return RT_FILE_NOT_FOUND;
+    std::unique_ptr<FILE, int (*)(FILE*)> guard(f, std::fclose);
+    char magic[8];
+    uint32_t hdr32[2];
+    uint64_t hdr64[3];
+    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kSceneMagic, 8) != 0) return RT_PARSE_ERROR;
+    if (std::fread(hdr32, sizeof(hdr32), 1, f) != 1 || hdr32[0] != kSceneVersion) return RT_PARSE_ERROR;
+    if (std::fread(hdr64, sizeof(hdr64), 1, f) != 1) return RT_PARSE_ERROR;
+    // sizes must match the file before anything is allocated
+    if (std::fseek(f, 0, SEEK_END) != 0) return RT_PARSE_ERROR;
+    const long fsize = std::ftell(f);
+    const uint64_t body = hdr64[0] * sizeof(rt_cl_triangle) + hdr64[1] * sizeof(rt_cl_bvh_node) +
+                          hdr64[2] * sizeof(rt_cl_material);
+    if (hdr64[0] > (1ull << 32) || hdr64[1] > (1ull << 32) || hdr64[2] > (1ull << 32) || fsize < 0 ||
+        (uint64_t)fsize != 8 + sizeof(hdr32) + sizeof(hdr64) + body + 8)
+        return RT_PARSE_ERROR;
+    if (std::fseek(f, 8 + sizeof(hdr32) + sizeof(hdr64), SEEK_SET) != 0) return RT_PARSE_ERROR;
+    std::unique_ptr<rt_scene> s(new (std::nothrow) rt_scene());
+    if (!s) return RT_OUT_OF_HOST_MEMORY;
+    s->tris.resize(hdr64[0]);
+    s->nodes.resize(hdr64[1]);
+    s->mats.resize(hdr64[2]);
+    s->max_prims = hdr32[1];
+    uint64_t stored = 0;
+    bool ok = std::fread(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size(), f) == s->tris.size();
+    ok = ok && std::fread(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size(), f) == s->nodes.size();
+    ok = ok && std::fread(s->mats.data(), sizeof(rt_cl_material), s->mats.size(), f) == s->mats.size();
+    ok = ok && std::fread(&stored, sizeof(stored), 1, f) == 1;
+    if (!ok) return RT_PARSE_ERROR;
+    uint64_t h = 14695981039346656037ull;
+    h = fnv1a(kSceneMagic, 8, h);
+    h = fnv1a(hdr32, sizeof(hdr32), h);
+    h = fnv1a(hdr64, sizeof(hdr64), h);
+    h = fnv1a(s->tris.data(), s->tris.size() * sizeof(rt_cl_triangle), h);
+    h = fnv1a(s->nodes.data(), s->nodes.size() * sizeof(rt_cl_bvh_node), h);
+    h = fnv1a(s->mats.data(), s->mats.size() * sizeof(rt_cl_material), h);
+    if (h != stored) return RT_PARSE_ERROR;
+    if (check_arrays(s->nodes, s->tris.size())) return RT_PARSE_ERROR;
+    *out = s.release();
+    return RT_SUCCESS;
+}
+
 void rtsRelease(rt_scene* s) { delete s; }
 
 }  // extern "C"

@@ -179,3 +179,35 @@ def test_loader_reproduces_committed_fixture():
         if key in z.files:
             h = hashlib.sha256(open(os.path.join(REF, fn), "rb").read()).digest()
             assert z[key].tobytes() == h
+
+
+def test_binary_scene_cache_roundtrip(tmp_path, cornell):
+    """rtsSaveScene / rtsLoadScene: byte-identical arrays back; corruption and
+    truncation are RT_PARSE_ERROR, a missing file RT_FILE_NOT_FOUND."""
+    p = str(tmp_path / "c.rtscene")
+    S.save_scene(cornell, p)
+    back = S.load_scene(p)
+    for a, b in ((cornell.triangles, back.triangles), (cornell.nodes, back.nodes),
+                 (cornell.materials, back.materials)):
+        assert a.tobytes() == b.tobytes()
+    raw = bytearray(open(p, "rb").read())
+    raw[200] ^= 1
+    bad = tmp_path / "bad.rtscene"
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(N.RTError) as e:
+        S.load_scene(str(bad))
+    assert e.value.code == -1002
+    (tmp_path / "short.rtscene").write_bytes(bytes(raw[:-9]))
+    with pytest.raises(N.RTError) as e:
+        S.load_scene(str(tmp_path / "short.rtscene"))
+    assert e.value.code == -1002
+    with pytest.raises(N.RTError) as e:
+        S.load_scene(str(tmp_path / "none.rtscene"))
+    assert e.value.code == RT_FILE_NOT_FOUND
+
+
+def test_from_arrays_rejects_broken_trees(cornell):
+    nodes = cornell.nodes.copy()
+    nodes[0]["offset"] = 0  # second child before the first
+    with pytest.raises(N.RTError):
+        S.save_scene(S.Scene(cornell.triangles, nodes, cornell.materials), "/tmp/never_written.rtscene")
