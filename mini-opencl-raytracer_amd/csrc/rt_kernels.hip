@@ -201,6 +201,25 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
     return false;
 }
 
+// LDS octant record visit returning the raw hit_next word on entering a leaf.
+__device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                          float t, uint32_t& next, uint32_t& leaf_code) {
+    const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
+    const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
+    const bool hit = t1 >= t0;
+    const bool leaf = hit && (hn & kLeafBit);
+    next = (hit && !leaf) ? hn : mn;
+    leaf_code = hn;
+    return leaf;
+}
+
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
 // early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
 // ones the reference computes where it reaches them; the rest are discarded.  A wave
@@ -819,7 +838,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (state == kTrav) {
                         if (kStats) ++st.visits;
                         uint32_t next, first = 0, count = 0;
-                        if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
+                        if (kLdsScene) {
+                            // LDS records: the LEAF state keeps the packed leaf word itself
+                            // (bit 31 | count-1 << 24 | first); the triangle steps walk it
+                            uint32_t code;
+                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
+                                state = kLeaf;
+                                leaf_i = code;
+                            }
+                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
                             state = kLeaf;
                             leaf_i = first;
                             leaf_end = first + count;
@@ -833,9 +860,16 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 for (int rep = 0; rep < kTriBurst; ++rep) {
                     if (state == kLeaf) {
                         if (kStats) ++st.tests;
-                        ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                        ++leaf_i;
-                        if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
+                        if (kLdsScene) {
+                            const uint32_t idx = leaf_i & 0x00ffffffu;
+                            ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
+                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kShade : kTrav;
+                            leaf_i += 1u - (1u << 24);
+                        } else {
+                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                            ++leaf_i;
+                            if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
+                        }
                     }
                 }
             }
