@@ -374,7 +374,7 @@ int prepare_scene(rt_kernel k) {
     }
     rc = ensure_dev(k->shade_tris, k->shade_tris_cap, (size_t)nt * 3);
     if (rc) return rc;
-    rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 3);
+    rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 4);
     if (rc) return rc;
     hipError_t e = rtk::launch_pack(static_cast<const rt_cl_bvh_node*>(nm->dptr), nn, k->packed_nodes,
                                     static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
@@ -665,8 +665,8 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.stats = k->dstats;
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
-    // (48 B per triangle, 48 B per material); no stack
-    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 48;
+    // (48 B per triangle, 64 B per material); no stack
+    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
     const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +

@@ -99,7 +99,7 @@ struct SceneView {
     const uint32_t* skips;  // global path: [node][octant] next node in the octant's DFS order
     const float4* onodes;   // LDS path: octant-resolved node records
     const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, -}, {n3, -}
-    const float4* smats;    // per material: {diffuse, roughness}, {specular, -}, {emission, -}
+    const float4* smats;    // per material: {diffuse, roughness}, {specular, alpha}, {emission, 1/(alpha+1)}, {alpha^2/pi, alpha^2-1}
 };
 
 constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
@@ -118,7 +118,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
         for (uint32_t i = tid; i < 16 * a.nNodes; i += 256) lo[i] = a.octNodes[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
-        for (uint32_t i = tid; i < 3 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
+        for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
         __syncthreads();
         return SceneView{nullptr, lt, nullptr, lo, ls, lm};
     }
@@ -132,7 +132,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kLdsScene ? 16u * a.nNodes + 6u * a.nTris + 3u * a.nMats : 4u * a.nTop;
+    return kLdsScene ? 16u * a.nNodes + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -303,7 +303,10 @@ __device__ __forceinline__ void onb(F3 n, F3& s, F3& t) {
 
 struct MatView {
     F3 diffuse, specular, emission;
-    float roughness;
+    // GGX constants of the material, formed once per material by pack_mats with the
+    // reference's operations (kernel_bvh.cl:229, :233, :283): alpha = 2/roughness^2 - 2,
+    // 1/(alpha + 1), alpha^2 * (1/pi), alpha^2 - 1
+    float alpha, inv_a1, a2pi, a2m1;
 };
 
 // SampleBrdf (kernel_bvh.cl:294-302) with SampleSpecular (:271-292) and SampleDiffuse
@@ -319,15 +322,14 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
                                           uint32_t& seed) {
     const bool spec = next_rand(seed) > 0.5f;
     const float phi = kTwoPi * next_rand(seed);
-    float alpha = 0.0f, sinT, c;
+    float sinT, c;
     if (spec) {
-        alpha = 2.0f / M::pow2(m.roughness) - 2.0f;
         (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
         const float r = next_rand(seed);
 #ifdef RT_EXP_NO_BRDF_POW
-        c = r * (1.0f / (alpha + 1.0f));  // timing experiment only (not the reference)
+        c = r * m.inv_a1;  // timing experiment only (not the reference)
 #else
-        c = M::pow(r, 1.0f / (alpha + 1.0f));  // cosTheta
+        c = M::pow(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
 #endif
         sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - c * c));
     } else {
@@ -350,8 +352,7 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
         const float cosTheta = c;
         wi = (-wo) + wh * (2.0f * M::dot(wo, wh));
         if (M::dot(wi, n) * M::dot(wo, n) < 0.000001f) return f3s(0.0f);
-        const float a2 = alpha * alpha;
-        const float D = (a2 * kInvPi) / M::pow2(cosTheta * cosTheta * (a2 - 1.0f) + 1.0f);
+        const float D = m.a2pi / M::pow2(cosTheta * cosTheta * m.a2m1 + 1.0f);
         pdf = (D * cosTheta) / (4.0f * M::max(M::dot(wo, wh), 0.0f));
         const float denom =
             (4.0f * M::max(M::dot(wi, n), 0.0f)) * M::max(M::dot(wo, n), 0.0f) + 0.001f;
@@ -408,9 +409,9 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
     const F3 normal = normalize<M>((F3{s2.x, s2.y, s2.z} * h.u + F3{s3.x, s3.y, s3.z} * h.v) +
                                    F3{s1.x, s1.y, s1.z} * w);
     const F3 pos = ray.o + ray.d * h.t;
-    const uint32_t mi = 3u * __float_as_uint(s1.w);
-    const float4 m0 = sc.smats[mi], m1 = sc.smats[mi + 1], m2 = sc.smats[mi + 2];
-    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m0.w};
+    const uint32_t mi = 4u * __float_as_uint(s1.w);
+    const float4 m0 = sc.smats[mi], m1 = sc.smats[mi + 1], m2 = sc.smats[mi + 2], m3 = sc.smats[mi + 3];
+    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m1.w, m2.w, m3.x, m3.y};
 
     radiance = radiance + (beta * m.emission) * 50.0f;
     F3 wi = f3s(0.0f);
@@ -1377,9 +1378,12 @@ __global__ void pack_mats(const rt_cl_material* __restrict__ in, float4* __restr
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const rt_cl_material& m = in[i];
-    out[3 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, m.roughness);
-    out[3 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, 0.0f);
-    out[3 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, 0.0f);
+    const float alpha = 2.0f / (m.roughness * m.roughness) - 2.0f;  // pow(r, 2.0f) == r * r
+    const float a2 = alpha * alpha;
+    out[4 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, m.roughness);
+    out[4 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, alpha);
+    out[4 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, 1.0f / (alpha + 1.0f));
+    out[4 * i + 3] = make_float4(a2 * kInvPi, a2 - 1.0f, 0.0f, 0.0f);
 }
 
 __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
