@@ -177,6 +177,23 @@ RT_PM_FN float pm_cos(float x) {
     if (pm_isnan(x) || pm_isinf(x)) return pm_u2f(0x7fc00000u);
     return (float)pm_cos_d((double)x);
 }
+/* sin and cos of one argument from one reduction: the same operations as pm_sin / pm_cos,
+ * so the same bits, for half the reduction work */
+RT_PM_FN void pm_sincos(float x, float* s, float* c) {
+    if (pm_isnan(x) || pm_isinf(x)) {
+        *s = *c = pm_u2f(0x7fc00000u);
+        return;
+    }
+    double r;
+    const int q = pm_reduce_pio2((double)x, &r);
+    const double ks = pm_ksin(r), kc = pm_kcos(r);
+    switch (q) {
+        case 0: *s = (float)ks; *c = (float)kc; break;
+        case 1: *s = (float)kc; *c = (float)(-ks); break;
+        case 2: *s = (float)(-ks); *c = (float)(-kc); break;
+        default: *s = (float)(-kc); *c = (float)ks; break;
+    }
+}
 RT_PM_FN float pm_tan(float x) {
     if (pm_isnan(x) || pm_isinf(x)) return pm_u2f(0x7fc00000u);
     double xd = (double)x;

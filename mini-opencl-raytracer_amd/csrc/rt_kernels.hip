@@ -343,8 +343,10 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     const F3 pa = (s * (1.0f - phi)) * sinT;  // timing experiment only (not the reference)
     const F3 pb = (t * phi) * sinT;
 #else
-    const F3 pa = (s * M::cos(phi)) * sinT;
-    const F3 pb = (t * M::sin(phi)) * sinT;
+    float sphi, cphi;
+    M::sincos(phi, sphi, cphi);
+    const F3 pa = (s * cphi) * sinT;
+    const F3 pb = (t * sphi) * sinT;
 #endif
     const F3 dir = normalize<M>((pa + pb) + n * c);
     if (spec) {

@@ -53,6 +53,7 @@ struct MathPinned {
     __device__ __forceinline__ static float pow2(float x) { return pm_sq(x); }
     __device__ __forceinline__ static float sin(float x) { return pm_sin(x); }
     __device__ __forceinline__ static float cos(float x) { return pm_cos(x); }
+    __device__ __forceinline__ static void sincos(float x, float& s, float& c) { pm_sincos(x, &s, &c); }
     __device__ __forceinline__ static float tan(float x) { return pm_tan(x); }
     __device__ __forceinline__ static float max(float x, float y) { return pm_max(x, y); }
     __device__ __forceinline__ static float min(float x, float y) { return pm_min(x, y); }
@@ -76,6 +77,9 @@ struct MathDeviceLib {
     __device__ __forceinline__ static float pow2(float x) { return x * x; }
     __device__ __forceinline__ static float sin(float x) { return ::sinf(x); }
     __device__ __forceinline__ static float cos(float x) { return ::cosf(x); }
+    // ocml's sincos runs sin's and cos's reduction and polynomials once: same bits as the
+    // two separate builtins the reference calls (checked against the reference kernel)
+    __device__ __forceinline__ static void sincos(float x, float& s, float& c) { ::sincosf(x, &s, &c); }
     __device__ __forceinline__ static float tan(float x) { return ::tanf(x); }
     __device__ __forceinline__ static float max(float x, float y) { return __builtin_fmaxf(x, y); }
     __device__ __forceinline__ static float min(float x, float y) { return __builtin_fminf(x, y); }

@@ -45,6 +45,8 @@ def lib() -> ctypes.CDLL:
         for name in ("oracle_sin", "oracle_cos", "oracle_tan"):
             getattr(L, name).argtypes = [ctypes.c_float]
             getattr(L, name).restype = ctypes.c_float
+        L.oracle_sincos_mismatches.argtypes = [ctypes.c_void_p, ctypes.c_long]
+        L.oracle_sincos_mismatches.restype = ctypes.c_long
         L.oracle_hash.argtypes = [ctypes.c_uint32]
         L.oracle_hash.restype = ctypes.c_uint32
         L.oracle_frame_hash.argtypes = [ctypes.c_uint32]

@@ -460,6 +460,17 @@ float oracle_pow(float x, float y) { return pm_pow(x, y); }
 float oracle_sin(float x) { return pm_sin(x); }
 float oracle_cos(float x) { return pm_cos(x); }
 float oracle_tan(float x) { return pm_tan(x); }
+/* number of inputs where pm_sincos differs (bitwise) from pm_sin / pm_cos */
+long oracle_sincos_mismatches(const float* xs, long n) {
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+        float s, c;
+        pm_sincos(xs[i], &s, &c);
+        const float s1 = pm_sin(xs[i]), c1 = pm_cos(xs[i]);
+        if (pm_f2u(s) != pm_f2u(s1) || pm_f2u(c) != pm_f2u(c1)) ++bad;
+    }
+    return bad;
+}
 float oracle_max(float x, float y) { return pm_max(x, y); }
 float oracle_min(float x, float y) { return pm_min(x, y); }
 

@@ -74,6 +74,16 @@ def test_pinned_trig(oracle_mod):
     assert L.oracle_tan(a) == f32(math.tan(a))
 
 
+def test_pinned_sincos_equals_sin_and_cos(oracle_mod):
+    """pm_sincos (one reduction, used by the kernels) == pm_sin / pm_cos bit for bit."""
+    L = oracle_mod.lib()
+    rng = np.random.default_rng(11)
+    xs = np.concatenate([rng.uniform(0.0, 6.2831855, 2_000_000), rng.uniform(-1e6, 1e6, 200_000),
+                         [0.0, -0.0, 1e-30, np.pi / 2, np.pi, 3 * np.pi / 2, 2 * np.pi, 1e30, np.inf,
+                          -np.inf, np.nan]]).astype(np.float32)
+    assert L.oracle_sincos_mismatches(xs.ctypes.data, xs.size) == 0
+
+
 def test_pinned_max_min_rules(oracle_mod):
     L = oracle_mod.lib()
     nan = float("nan")
