@@ -74,14 +74,15 @@ __device__ __forceinline__ Ray init_ray(F3 o, F3 d) {
 }
 
 // kernel_bvh.cl:386-403
+// (px, py) = (gid % W, gid / W), passed in by the callers that already know them.
 template <class M>
-__device__ __forceinline__ Ray create_ray(uint32_t gid, uint32_t W, uint32_t H, F3 pos, F3 front,
+__device__ __forceinline__ Ray create_ray(uint32_t px, uint32_t py, uint32_t W, uint32_t H, F3 pos, F3 front,
                                           F3 up, float angle, uint32_t& seed) {
     const float invW = 1.0f / (float)W;
     const float invH = 1.0f / (float)H;
     const float aspect = (float)W / (float)H;
-    float x = ((float)(gid % W) + next_rand(seed)) - 0.5f;
-    float y = ((float)(gid / W) + next_rand(seed)) - 0.5f;
+    float x = ((float)px + next_rand(seed)) - 0.5f;
+    float y = ((float)py + next_rand(seed)) - 0.5f;
     x = ((2.0f * ((x + 0.5f) * invW) - 1.0f) * angle) * aspect;
     y = -(1.0f - 2.0f * ((y + 0.5f) * invH)) * angle;
     F3 dir = ((M::cross(front, up) * x) + (up * y)) + front;
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
         const uint32_t gid = (uint32_t)g64;
 
         uint32_t seed = gid + fh;  // kernel_bvh.cl:445
-        const Ray ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+        const Ray ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
         int32_t pid = -1;
         float pt = 0.0f;
         const F3 rad = render<M, kLdsScene, kStats>(sc, ray, seed, a, pid, pt, st);
@@ -584,8 +585,8 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
             if (!active && rank < take) {
-                const uint32_t idx = chunk_base + chunk_used + rank;
-                const uint32_t tile = idx >> 6, w = idx & 63u;
+                const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
+                const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
                 const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                 const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
                 if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                     gid = (uint32_t)g64;
                     seed = gid + fh;  // kernel_bvh.cl:445
-                    ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+                    ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
                     radiance = f3s(0.0f);
                     beta = f3s(1.0f);
                     bounce = 0;
@@ -769,8 +770,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
                 if (state == kIdle && rank < take) {
-                    const uint32_t idx = chunk_base + chunk_used + rank;
-                    const uint32_t tile = idx >> 6, w = idx & 63u;
+                    const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
+                    const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -778,7 +779,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;
                         seed = gid + fh;  // kernel_bvh.cl:445
-                        ray = create_ray<M>(gid, a.width, a.height, camPos, camFront, camUp, angle, seed);
+                        ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
                         radiance = f3s(0.0f);
                         beta = f3s(1.0f);
                         bounce = 0;
@@ -1180,8 +1181,8 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                     const uint32_t rank = lane_rank(idle);
                     const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
                     if (state == kIdle && rank < take) {
-                        const uint32_t idx = chunk_base + chunk_used + rank;
-                        const uint32_t tile = idx >> 6, w = idx & 63u;
+                        const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
+                        const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
                         const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                         const uint32_t x = tx * 8u + (w & 7u),
                                        row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -1189,7 +1190,7 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                         if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                             ps.gid = (uint32_t)g64;
                             ps.seed = ps.gid + fh;  // kernel_bvh.cl:445
-                            ray = create_ray<M>(ps.gid, a.width, a.height, camPos, camFront, camUp, angle, ps.seed);
+                            ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, ps.seed);
                             ps.radiance = f3s(0.0f);
                             ps.beta = f3s(1.0f);
                             ps.bounce = 0;
