@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--bounces", type=int, default=9)
     p.add_argument("--math", choices=["pinned", "devicelib"], default="devicelib")
+    p.add_argument("--bvh", choices=["host", "device"], default="host",
+                   help="host: the reference's SAH build (default); device: rtBuildBVH linear BVH")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
     p.add_argument("--sched", choices=["regen", "tiles", "step", "pool"], default="step")
@@ -161,6 +163,14 @@ def main():
         scene = clrt_proxy.bunny_proxy()
     else:
         scene = clrt.scene.cornell()
+    if args.bvh == "device":  # linear BVH built on the GPU (rtBuildBVH)
+        if args.scene == "bunny":
+            raw = clrt.scene.load_obj(os.path.join(clrt_proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
+            ft, fm = raw.triangles, raw.materials
+        else:
+            z = np.load(clrt.scene.CORNELL_NPZ, allow_pickle=False)
+            ft, fm = z["triangles"].view(N.TRIANGLE_DTYPE), z["materials"].view(N.MATERIAL_DTYPE)
+        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=device)
     r = Rank(scene, args, device, rank, world)
 
     # instrumented pass: ray / node / triangle / hit counts of one step on this rank
@@ -269,7 +279,7 @@ def main():
                  "generated bunny-class proxy OBJ (clrt/proxy.py)") + "; rays generated in-kernel",
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "schedule": args.sched, "parallelism": f"interleaved 8-row bands x{world}" + (
+                   "math": args.math, "schedule": args.sched, "bvh": args.bvh, "parallelism": f"interleaved 8-row bands x{world}" + (
                        (" + RCCL gather to rank 0" if args.dist_backend == "nccl" else " + gloo gather to rank 0 (host-staged)")
                        if world > 1 else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},

@@ -123,6 +123,16 @@ int rtKernelSetMathMode(rt_kernel k, int mode);
 #define RT_SCHED_POOL 3
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
+/* Device-side BVH build (extension): a linear BVH (Morton codes, radix
+ * tree) over the `n_tris` CLTriangle records of `tris` (file order), for meshes too large to
+ * build on the host quickly.  Permutes `tris` in place into leaf order and writes the
+ * depth-first CLLinearBVHNode[] into `nodes` (capacity >= (2*n_tris - 1) * 48 bytes), count
+ * in *n_nodes -- the node contract of CLBVHnode.cpp:161-183, so the buffers bind to
+ * KernelEntry as they are.  The tree is not the host SAH tree (hit IDs may differ where
+ * triangles tie). */
+int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, rt_mem nodes,
+               size_t* n_nodes);
+
 /* Restrict the next launches to work-items [first, last) (pixel-row tiles for
  * multi-GPU sharding); last = 0 means "to global_work_size".  Work-item ids, and
  * therefore seeds and output slots, stay global. */

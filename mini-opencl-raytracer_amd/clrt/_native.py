@@ -111,6 +111,7 @@ _HIP_PROTOS = {
     "rtKernelResetStats": (ctypes.c_int, [_vp]),
     "rtKernelGetSceneInLDS": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "rtKernelForceGlobalScene": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtBuildBVH": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint, _vp, ctypes.POINTER(ctypes.c_size_t)]),
     "rtBufferGetDevicePointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "rtBufferGetSize": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
     "rtContextGetStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),

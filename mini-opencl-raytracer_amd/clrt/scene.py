@@ -92,6 +92,30 @@ def build_bvh(triangles: np.ndarray, materials: np.ndarray, max_prims_in_node: i
     return Scene(t, n, m, max_prims_in_node)
 
 
+def build_bvh_device(triangles: np.ndarray, materials: np.ndarray, max_prims_in_node: int = 4,
+                     device: int = 0) -> Scene:
+    """Device-side BVH build (rtBuildBVH): same array contract as build_bvh,
+    a linear BVH instead of the reference's SAH tree.  Needs a GPU."""
+    from . import _native as N
+    from .device import CLContext
+    tris = np.ascontiguousarray(triangles, dtype=TRIANGLE_DTYPE)
+    n = tris.shape[0]
+    ctx = CLContext(device)
+    try:
+        tb = ctx.create_buffer(N.MEM_READ_WRITE | N.MEM_COPY_HOST_PTR, tris.nbytes, tris)
+        nb = ctx.create_buffer(N.MEM_READ_WRITE, max(1, 2 * n - 1) * NODE_DTYPE.itemsize)
+        count = ctx.BuildBVH(tb, n, max_prims_in_node, nb)
+        out_t = np.empty_like(tris)
+        out_n = np.empty(count, NODE_DTYPE)
+        ctx.ReadBuffer(tb, out_t, blocking=True)
+        ctx.ReadBuffer(nb, out_n, out_n.nbytes, blocking=True)
+        tb.release()
+        nb.release()
+    finally:
+        ctx.release()
+    return Scene(out_t, out_n, np.ascontiguousarray(materials, dtype=MATERIAL_DTYPE), max_prims_in_node)
+
+
 def save_scene(scene: Scene, path: str) -> None:
     """Binary scene cache (rtsSaveScene): the three arrays exactly as built."""
     lib = scene_lib()

@@ -23,6 +23,7 @@
 
 #include "../../include/rt_cl_types.h"
 #include "../../include/rt_hip.h"
+#include "rt_bvh.hpp"
 #include "rt_kernels.hpp"
 
 namespace {
@@ -706,6 +707,32 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
         }
     }
     ++k->launches;
+    return RT_SUCCESS;
+}
+
+int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, rt_mem nodes,
+               size_t* n_nodes) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    if (!tris || !nodes || tris->ctx != ctx || nodes->ctx != ctx) return RT_INVALID_MEM_OBJECT;
+    if (!n_nodes || n_tris == 0 || n_tris >= (1u << 30)) return RT_INVALID_VALUE;
+    if (tris->size < n_tris * sizeof(rt_cl_triangle)) return RT_INVALID_BUFFER_SIZE;
+    if (nodes->size < (2 * n_tris - 1) * sizeof(rt_cl_bvh_node)) return RT_INVALID_BUFFER_SIZE;
+    const uint32_t mp = std::max(1u, std::min(max_prims_in_node, 65535u));
+    void* scratch = nullptr;
+    hipError_t e = hipMalloc(&scratch, rtb::scratch_bytes((uint32_t)n_tris));
+    if (e != hipSuccess) return map_hip(e);
+    uint32_t count = 0;
+    e = rtb::build(static_cast<rt_cl_triangle*>(tris->dptr), (uint32_t)n_tris, mp,
+                   static_cast<rt_cl_bvh_node*>(nodes->dptr), &count, scratch, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(scratch);
+    if (e != hipSuccess) return map_hip(e);
+    for (rt_mem m : {tris, nodes}) {  // device contents changed: host shadows are stale
+        m->shadow_valid = false;
+        ++m->generation;
+    }
+    *n_nodes = count;
     return RT_SUCCESS;
 }
 
