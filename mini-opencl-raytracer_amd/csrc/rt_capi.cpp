@@ -86,9 +86,7 @@ struct rt_kernel_s {
     // derived packed scene
     rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
-    float4* packed_nodes = nullptr;
     float4* packed_tris = nullptr;
-    uint32_t* packed_skips = nullptr;
     float4* oct_nodes = nullptr;       // [node][octant] 2 x float4 (LDS-resident scenes)
     float4* shade_tris = nullptr;      // compact shading records (normals + mtlIndex)
     float4* shade_mats = nullptr;      // compact materials
@@ -97,7 +95,7 @@ struct rt_kernel_s {
     float4* g_nodes = nullptr;         // global-scene node records (64 B, top of the tree first)
     size_t g_nodes_cap = 0;
     uint32_t n_top = 0, top_limit = 256;  // nodes of g_nodes staged in LDS (global path)
-    size_t packed_nodes_cap = 0, packed_tris_cap = 0, packed_skips_cap = 0, oct_nodes_cap = 0;
+    size_t packed_tris_cap = 0, oct_nodes_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
@@ -325,22 +323,6 @@ int prepare_scene(rt_kernel k) {
     std::vector<uint32_t> skips;
     build_skips(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips);
 
-    if (k->packed_nodes_cap < (size_t)nn) {
-        if (k->packed_nodes) (void)hipFree(k->packed_nodes);
-        k->packed_nodes = nullptr;
-        k->packed_nodes_cap = 0;
-        hipError_t e = hipMalloc(&k->packed_nodes, (size_t)nn * 2 * sizeof(float4));
-        if (e != hipSuccess) return map_hip(e);
-        k->packed_nodes_cap = nn;
-    }
-    if (k->packed_skips_cap < (size_t)nn) {
-        if (k->packed_skips) (void)hipFree(k->packed_skips);
-        k->packed_skips = nullptr;
-        k->packed_skips_cap = 0;
-        hipError_t e = hipMalloc(&k->packed_skips, (size_t)nn * 8 * sizeof(uint32_t));
-        if (e != hipSuccess) return map_hip(e);
-        k->packed_skips_cap = nn;
-    }
     if (nn >= (1u << 30)) return RT_INVALID_MEM_OBJECT;  // node indices share a word with the axis
     std::vector<uint32_t> gn;
     uint32_t n_top = 0;
@@ -357,11 +339,8 @@ int prepare_scene(rt_kernel k) {
     rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)nn * 16);
     if (rc) return rc;
     {
-        hipError_t e = hipMemcpyAsync(k->packed_skips, skips.data(), skips.size() * sizeof(uint32_t),
+        hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
                                       hipMemcpyHostToDevice, k->ctx->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                               k->ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
         if (e != hipSuccess) return map_hip(e);
     }
@@ -377,8 +356,7 @@ int prepare_scene(rt_kernel k) {
     if (rc) return rc;
     rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 4);
     if (rc) return rc;
-    hipError_t e = rtk::launch_pack(static_cast<const rt_cl_bvh_node*>(nm->dptr), nn, k->packed_nodes,
-                                    static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
+    hipError_t e = rtk::launch_pack(static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
                                     k->shade_tris, static_cast<const rt_cl_material*>(mm->dptr), nmat,
                                     k->shade_mats, k->ctx->stream);
     if (e != hipSuccess) return map_hip(e);
@@ -554,9 +532,7 @@ int rtReleaseKernel(rt_kernel k) {
         (void)hipEventDestroy(pr.second);
     }
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
-    if (k->packed_nodes) (void)hipFree(k->packed_nodes);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
-    if (k->packed_skips) (void)hipFree(k->packed_skips);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
     if (k->g_nodes) (void)hipFree(k->g_nodes);
     if (k->shade_tris) (void)hipFree(k->shade_tris);
@@ -614,9 +590,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.result = static_cast<float4*>(out->dptr);
     a.trisFull = static_cast<const rt_cl_triangle*>(k->bufs[RT_ARG_BUFFER_SCENE]->dptr);
     a.materials = static_cast<const rt_cl_material*>(k->bufs[RT_ARG_BUFFER_MATERIAL]->dptr);
-    a.packedNodes = k->packed_nodes;
     a.packedTris = k->packed_tris;
-    a.skips = k->packed_skips;
     a.octNodes = k->oct_nodes;
     a.gNodes = k->g_nodes;
     a.shadeTris = k->shade_tris;

@@ -95,10 +95,9 @@ __device__ __forceinline__ Ray create_ray(uint32_t px, uint32_t py, uint32_t W, 
 // LDS scenes: octant-resolved records A[octant][node] = {near.xyz, far.x}, B[octant][node] =
 // {far.yz, hit_next, miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
 struct SceneView {
-    const float4* nodes;    // global path: 64-B records (generic pointer: the top in LDS)
+    const float4* nodes;    // global path: 64-B node records (bounds, children, 8 skip pointers)
     const float4* tris;     // LDS or global
-    const uint32_t* skips;  // global path: [node][octant] next node in the octant's DFS order
-    const float4* onodes;   // LDS path: octant-resolved node records
+    const float4* onodes;   // LDS path: octant-resolved node records; global path: the LDS top
     const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, -}, {n3, -}
     const float4* smats;    // per material: {diffuse, roughness}, {specular, alpha}, {emission, 1/(alpha+1)}, {alpha^2/pi, alpha^2-1}
 };
@@ -121,13 +120,13 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
         for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
         __syncthreads();
-        return SceneView{nullptr, lt, nullptr, lo, ls, lm};
+        return SceneView{nullptr, lt, lo, ls, lm};
     }
     // global scene: the top-of-tree node records into LDS, the rest read from HBM/L2
     const int tid = threadIdx.x;
     for (uint32_t i = tid; i < 4 * a.nTop; i += 256) smem[i] = a.gNodes[i];
     __syncthreads();
-    return SceneView{a.gNodes, a.packedTris, nullptr, smem, a.shadeTris, a.shadeMats};
+    return SceneView{a.gNodes, a.packedTris, smem, a.shadeTris, a.shadeMats};
 }
 
 // LDS float4s of the scene (the finish queue / pool follow it)
@@ -327,11 +326,7 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     if (spec) {
         (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
         const float r = next_rand(seed);
-#ifdef RT_EXP_NO_BRDF_POW
-        c = r * m.inv_a1;  // timing experiment only (not the reference)
-#else
         c = M::pow(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
-#endif
         sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - c * c));
     } else {
         const float s2 = next_rand(seed);
@@ -340,15 +335,10 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     }
     F3 s, t;
     onb<M>(n, s, t);
-#ifdef RT_EXP_NO_TRIG
-    const F3 pa = (s * (1.0f - phi)) * sinT;  // timing experiment only (not the reference)
-    const F3 pb = (t * phi) * sinT;
-#else
     float sphi, cphi;
     M::sincos(phi, sphi, cphi);
     const F3 pa = (s * cphi) * sinT;
     const F3 pb = (t * sphi) * sinT;
-#endif
     const F3 dir = normalize<M>((pa + pb) + n * c);
     if (spec) {
         const F3 wh = dir;
@@ -457,15 +447,9 @@ __device__ __forceinline__ void finish_color(const KernelArgs& a, uint32_t gid, 
     } else {
         const float4 old = a.result[gid];
         const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
-#ifdef RT_EXP_NO_GAMMA
-        const F3 lin{old.x * old.x, old.y * old.y, old.z * old.z};  // timing experiment only
-        const F3 acc = ((lin * fm1) + rad) / fc;
-        out = acc;
-#else
         const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
         const F3 acc = ((lin * fm1) + rad) / fc;
         out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
-#endif
     }
     a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
 }
@@ -1358,16 +1342,6 @@ __global__ __launch_bounds__(256) RT_POOL_PINNED_OCC void kernel_entry_pool_pinn
 }
 
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
-__global__ void pack_nodes(const rt_cl_bvh_node* __restrict__ in, float4* __restrict__ out, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rt_cl_bvh_node nd = in[i];
-    const uint32_t meta = (uint32_t)nd.nPrimitives | ((uint32_t)(nd.nPrimitives ? 0 : nd.axis) << 16);
-    out[2 * i] = make_float4(nd.bounds.pmin.x, nd.bounds.pmin.y, nd.bounds.pmin.z, nd.bounds.pmax.x);
-    out[2 * i + 1] = make_float4(nd.bounds.pmax.y, nd.bounds.pmax.z, __uint_as_float(nd.offset),
-                                 __uint_as_float(meta));
-}
-
 __global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1443,10 +1417,8 @@ int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t sme
     return blocks > 0 ? blocks : 1;
 }
 
-hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
-                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
+hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
-    if (n_nodes) hipLaunchKernelGGL(pack_nodes, dim3((n_nodes + 255) / 256), dim3(256), 0, st, nodes, pn, n_nodes);
     if (n_tris) hipLaunchKernelGGL(pack_tris, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, pt, n_tris);
     if (n_tris) hipLaunchKernelGGL(pack_shade, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, ps, n_tris);
     if (n_mats) hipLaunchKernelGGL(pack_mats, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);

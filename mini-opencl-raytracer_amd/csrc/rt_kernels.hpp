@@ -14,9 +14,7 @@ struct KernelArgs {
     float4* result;                     // slot 0: float3 per work-item, 16-byte stride
     const rt_cl_triangle* trisFull;     // slot 1 (normals, material index)
     const rt_cl_material* materials;    // slot 3
-    const float4* packedNodes;          // derived from slot 2: 2 x float4 per node
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
-    const uint32_t* skips;              // derived from slot 2: [node][octant] DFS skip pointers
     const float4* octNodes;             // derived from slot 2: [node][octant] resolved records (LDS path)
     const float4* gNodes;               // derived from slot 2: 64-B node records (global path)
     const float4* shadeTris;            // derived from slot 1: {n1, mtlIndex}, {n2}, {n3} per triangle
@@ -55,8 +53,7 @@ constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);
 int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
-hipError_t launch_pack(const rt_cl_bvh_node* nodes, uint32_t n_nodes, float4* pn,
-                       const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
+hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk
