@@ -73,6 +73,9 @@ struct rt_kernel_s {
     uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
+    uint32_t chunk_pixels = 128, tail_chunk = 64;  // pixels per work-counter fetch: bulk, tail
+    uint32_t bulk_percent = 80;                // share of the frame handed out in bulk chunks
+                                               // (swept on MI355X: profiles/r01/chunk_sweep.txt)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint64_t range_first = 0, range_last = 0;
@@ -502,6 +505,11 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
+    if (const char* v = std::getenv("RT_CHUNK"))
+        k->chunk_pixels = (uint32_t)std::max(1, std::min(64, std::atoi(v) / 64)) * 64u;
+    if (const char* v = std::getenv("RT_TAIL_CHUNK"))
+        k->tail_chunk = (uint32_t)std::max(1, std::min(64, std::atoi(v) / 64)) * 64u;
+    if (const char* v = std::getenv("RT_BULK_PERCENT")) k->bulk_percent = (uint32_t)std::max(0, std::min(100, std::atoi(v)));
     if (const char* v = std::getenv("RT_TOP_NODES")) k->top_limit = (uint32_t)std::max(0, std::min(1024, std::atoi(v)));
     if (const char* v = std::getenv("RT_POOL_SHADE")) k->pool_shade = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_PARK_MIN")) k->park_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
@@ -628,6 +636,12 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     if (n_tiles * 64 > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
     a.workCounter = k->work_counter;
+    a.chunkPixels = k->chunk_pixels;
+    a.tailChunk = k->tail_chunk;
+    {
+        const uint64_t tot = (uint64_t)a.nTiles * 64u;
+        a.chunkSplit = (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels);
+    }
     a.refillMin = k->refill_min;
     a.shadeMin = k->shade_min;
     a.stepWeightNode = k->w_node;

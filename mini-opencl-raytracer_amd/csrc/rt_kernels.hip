@@ -517,6 +517,32 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
     if (kStats) flush_stats(a, st, lane);
 }
 
+// Work distribution of the persistent schedules (guided self-scheduling): pixels are handed
+// out in chunks of whole 8x8 tiles from two global counters -- chunks of a.chunkPixels over the
+// first a.chunkSplit pixels, then chunks of a.tailChunk.  Large chunks keep the returning
+// atomics per frame low (one counter saturates near 90 per microsecond on MI355X); small
+// ones at the end keep the last waves from finishing alone.  Returns false when no work is left.
+__device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
+                                           uint32_t& len, bool& tail) {
+    uint32_t b = 0;
+    if (!tail) {
+        if (lane == 0) b = atomicAdd(&a.workCounter[0], a.chunkPixels);
+        b = __shfl(b, 0, 64);
+        if (b < a.chunkSplit) {
+            base = b;
+            len = min(a.chunkPixels, a.chunkSplit - b);
+            return true;
+        }
+        tail = true;  // this wave never asks the bulk counter again
+    }
+    if (lane == 0) b = atomicAdd(&a.workCounter[1], a.tailChunk);
+    b = __shfl(b, 0, 64) + a.chunkSplit;
+    if (b >= total) return false;
+    base = b;
+    len = min(a.tailChunk, total - b);
+    return true;
+}
+
 // ---- path-regeneration schedule -------------------------------------------------------------
 // Same per-pixel computation, different scheduling: every lane of a persistent wave carries
 // one path; when a path ends (miss, pdf break, or lightBounces reached) the lane writes its
@@ -546,7 +572,10 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
     float pt = 0.0f;
     Ray ray{};
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
-    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
+    // one returning atomic per chunk, so the counter stays far from its throughput limit
+    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    bool chunk_tail = false;                                  // wave-uniform
     bool exhausted = false;                    // wave-uniform
 
     for (;;) {
@@ -554,23 +583,19 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
         while (!exhausted) {
             const unsigned long long idle = __ballot(!active);
             if (idle == 0ull) break;
-            if (chunk_used >= 64u) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(a.workCounter, 64u);
-                b = __shfl(b, 0, 64);
-                if (b >= total) {
+            if (chunk_used >= chunk_len) {
+                if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
                     exhausted = true;
                     break;
                 }
-                chunk_base = b;
                 chunk_used = 0;
             }
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+            const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
             if (!active && rank < take) {
-                const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
-                const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
+                const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
+                const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
                 const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                 const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -699,7 +724,10 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
     uint32_t cur = 0;  // TRAV: node to visit; LEAF: node to continue at after the leaf
     uint32_t leaf_i = 0, leaf_end = 0;
-    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
+    // one returning atomic per chunk, so the counter stays far from its throughput limit
+    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    bool chunk_tail = false;                                  // wave-uniform
     bool exhausted = false;                    // wave-uniform
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
@@ -739,23 +767,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             while (!exhausted) {
                 const unsigned long long idle = __ballot(state == kIdle);
                 if (idle == 0ull) break;
-                if (chunk_used >= 64u) {
-                    uint32_t b = 0;
-                    if (lane == 0) b = atomicAdd(a.workCounter, 64u);
-                    b = __shfl(b, 0, 64);
-                    if (b >= total) {
+                if (chunk_used >= chunk_len) {
+                    if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
                         exhausted = true;
                         break;
                     }
-                    chunk_base = b;
                     chunk_used = 0;
                 }
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+                const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
                 if (state == kIdle && rank < take) {
-                    const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
-                    const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
+                    const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
+                    const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -1077,7 +1101,10 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
     Ray ray{};
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
     uint32_t cur = 0, leaf_i = 0, leaf_end = 0;
-    uint32_t chunk_base = 0, chunk_used = 64;  // wave-uniform
+    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
+    // one returning atomic per chunk, so the counter stays far from its throughput limit
+    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    bool chunk_tail = false;                                  // wave-uniform
     bool exhausted = false;                    // wave-uniform
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1151,22 +1178,18 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                 while (!exhausted) {
                     const unsigned long long idle = __ballot(state == kIdle);
                     if (idle == 0ull) break;
-                    if (chunk_used >= 64u) {
-                        uint32_t b = 0;
-                        if (lane == 0) b = atomicAdd(a.workCounter, 64u);
-                        b = __shfl(b, 0, 64);
-                        if (b >= total) {
+                    if (chunk_used >= chunk_len) {
+                        if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
                             exhausted = true;
                             break;
                         }
-                        chunk_base = b;
                         chunk_used = 0;
                     }
                     const uint32_t rank = lane_rank(idle);
-                    const uint32_t take = min((uint32_t)__popcll(idle), 64u - chunk_used);
+                    const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
                     if (state == kIdle && rank < take) {
-                        const uint32_t w = chunk_used + rank;  // chunks are 64-aligned: one tile per chunk
-                        const uint32_t tile = chunk_base >> 6;  // wave-uniform (scalar division)
+                        const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
+                        const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
                         const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                         const uint32_t x = tx * 8u + (w & 7u),
                                        row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);

@@ -29,7 +29,9 @@ struct KernelArgs {
     // work decomposition: work-items [gidBegin, gidEnd), rows [rowBegin, rowEnd)
     uint64_t gidBegin, gidEnd;
     uint32_t rowBegin, rowCount, tilesX, nTiles;  // tiles: 16x16 (tile schedule) or 8x8 (regen)
-    uint32_t* workCounter;              // regen schedule: next 64-pixel chunk (zeroed per launch)
+    uint32_t* workCounter;              // persistent schedules: next chunk (zeroed per launch)
+    uint32_t chunkPixels, tailChunk;    // pixels per chunk (multiples of 64: whole 8x8 tiles), bulk / tail
+    uint32_t chunkSplit;                // bulk chunks cover pixels [0, chunkSplit) of the tile order
     uint32_t refillMin, shadeMin;       // step schedule batching thresholds (lanes)
     uint32_t stepWeightNode, stepWeightLeaf;  // step schedule: relative cost of node / triangle steps
     uint32_t bandPeriod, bandPhase;     // 8-row bands: this launch renders bands b % period == phase
