@@ -638,10 +638,6 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.workCounter = k->work_counter;
     a.chunkPixels = k->chunk_pixels;
     a.tailChunk = k->tail_chunk;
-    {
-        const uint64_t tot = (uint64_t)a.nTiles * 64u;
-        a.chunkSplit = (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels);
-    }
     a.refillMin = k->refill_min;
     a.shadeMin = k->shade_min;
     a.stepWeightNode = k->w_node;
@@ -670,8 +666,17 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
         k->occ_smem[si][mi][lds][k->stats] = smem;
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
-    grid = std::min<uint64_t>(grid, n_tiles);
+    // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
+    grid = std::min<uint64_t>(grid, k->sched == RT_SCHED_TILES ? n_tiles : (n_tiles + 3) / 4);
     if (grid == 0) grid = 1;
+    {
+        // bulk chunks only when every resident wave gets at least two of them; a small frame
+        // (512x512: ~40 pixels per wave) is handed out 64 pixels at a time
+        const uint64_t tot = (uint64_t)a.nTiles * 64u, waves = grid * 4u;
+        a.chunkSplit = tot >= 2u * waves * k->chunk_pixels
+                           ? (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels)
+                           : 0u;
+    }
 
     if (k->sched != RT_SCHED_TILES) {
         hipError_t me = hipMemsetAsync(k->work_counter, 0, 16, ctx->stream);

@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = false;                                  // wave-uniform
+    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
 
     for (;;) {
@@ -727,7 +727,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = false;                                  // wave-uniform
+    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
@@ -1104,7 +1104,7 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = false;                                  // wave-uniform
+    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
