@@ -70,7 +70,7 @@ struct rt_kernel_s {
     float f3[3][4] = {};              // slots 11..13
     int math = RT_MATH_DEVICELIB;
     int sched = RT_SCHED_STEP;
-    uint32_t refill_min = 16, shade_min = 48;  // step schedule thresholds (swept on MI355X)
+    uint32_t refill_min = 8, shade_min = 48;   // step schedule thresholds (swept on MI355X)
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
     uint32_t chunk_pixels = 128, tail_chunk = 64;  // pixels per work-counter fetch: bulk, tail

@@ -944,7 +944,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 // 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
 // (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
 #ifndef RT_STEP_DEVICELIB_WAVES
-#define RT_STEP_DEVICELIB_WAVES 6
+#define RT_STEP_DEVICELIB_WAVES 5
 #endif
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
