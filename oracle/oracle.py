@@ -45,6 +45,8 @@ def lib() -> ctypes.CDLL:
         for name in ("oracle_sin", "oracle_cos", "oracle_tan"):
             getattr(L, name).argtypes = [ctypes.c_float]
             getattr(L, name).restype = ctypes.c_float
+        L.oracle_pixel_cost_mt.argtypes = [ctypes.POINTER(OracleArgs), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_pixel_cost_mt.restype = ctypes.c_int
         L.oracle_sincos_mismatches.argtypes = [ctypes.c_void_p, ctypes.c_long]
         L.oracle_sincos_mismatches.restype = ctypes.c_long
         L.oracle_hash.argtypes = [ctypes.c_uint32]
@@ -59,6 +61,22 @@ def lib() -> ctypes.CDLL:
         L.oracle_ray_bounds.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+def pixel_cost(scene, width: int, height: int, frame_count: int = 1, light_bounces: int = 9, threads: int = 0):
+    """Per-pixel work estimate of one frame (uint32[H, W]): visits + 2 tests + 15 rays."""
+    L = lib()
+    camera = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+    tris = np.ascontiguousarray(scene.triangles)
+    nodes = np.ascontiguousarray(scene.nodes)
+    mats = np.ascontiguousarray(scene.materials)
+    cam = (ctypes.c_float * 12)(*camera[0], 0.0, *camera[1], 0.0, *camera[2], 0.0)
+    a = OracleArgs(tris.ctypes.data, nodes.ctypes.data, mats.ctypes.data, width, height,
+                   frame_count & 0xFFFFFFFF, light_bounces, 0, 1.0, cam)
+    result = np.zeros((width * height, 4), np.float32)
+    cost = np.zeros(width * height, np.uint32)
+    L.oracle_pixel_cost_mt(ctypes.byref(a), result.ctypes.data, cost.ctypes.data, threads or (os.cpu_count() or 1))
+    return cost.reshape(height, width)
 
 
 def render(scene, width: int, height: int, frame_count: int = 1, light_bounces: int = 9,

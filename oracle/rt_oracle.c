@@ -452,6 +452,39 @@ int oracle_render_mt(const oracle_args* a, float* result, uint32_t g0, uint32_t 
     return 0;
 }
 
+/* Per-pixel work estimate for load-balance modelling (scripts/balance_model.py):
+ * node visits + 2 * triangle tests + 15 * rays (the relative cost of a traversal step, a
+ * triangle step and a shading round per lane on the GPU kernel). */
+typedef struct { const oracle_args* a; float* result; uint32_t* cost; uint32_t g0, g1; } o_cost_job;
+
+static void* o_cost_worker(void* p) {
+    o_cost_job* j = (o_cost_job*)p;
+    o_scene sc;
+    o_make_scene(j->a, &sc);
+    for (uint32_t g = j->g0; g < j->g1; ++g) {
+        o_counts c = {0, 0, 0, 0};
+        o_kernel_entry(g, (of3*)j->result, &sc, j->a->width, j->a->height, j->a->frameCount, &c, NULL, NULL);
+        j->cost[g] = (uint32_t)(c.node_visits + 2 * c.tri_tests + 15 * c.rays);
+    }
+    return NULL;
+}
+
+int oracle_pixel_cost_mt(const oracle_args* a, float* result, uint32_t* cost, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    o_cost_job jobs[256];
+    pthread_t th[256];
+    const uint64_t n = (uint64_t)a->width * a->height;
+    for (int i = 0; i < threads; ++i) {
+        jobs[i].a = a; jobs[i].result = result; jobs[i].cost = cost;
+        jobs[i].g0 = (uint32_t)(n * (uint64_t)i / (uint64_t)threads);
+        jobs[i].g1 = (uint32_t)(n * (uint64_t)(i + 1) / (uint64_t)threads);
+        pthread_create(&th[i], NULL, o_cost_worker, &jobs[i]);
+    }
+    for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+    return 0;
+}
+
 /* Known-answer hooks for the unit tests. */
 uint32_t oracle_hash(uint32_t x) { return o_hash(&x); }
 uint32_t oracle_frame_hash(uint32_t x) { return o_frame_hash(x); }
