@@ -58,6 +58,12 @@ def parse():
     p.add_argument("--sched", choices=["regen", "tiles", "step", "pool"], default="step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-overlap", action="store_true",
+                   help="N>1 nccl: gather after each step with a host sync instead of pipelining it")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the N>1 flow even at WORLD_SIZE 1 (exercises the RCCL path on one GPU)")
+    p.add_argument("--check-gather", action="store_true",
+                   help="after timing, check rank 0's bands in the gathered image (pipelined nccl)")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo = dry run of the N>1 flow (host-staged gather; ranks may share a GPU)")
     return p.parse_args()
@@ -146,7 +152,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch
         import torch.distributed as dist_mod
         if args.dist_backend == "nccl":
@@ -177,26 +183,64 @@ def main():
     st = count_pass(r)
     counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
 
-    gather = None
+    gather = land_all = None
+    final = None
     if dist is not None:
         import torch
-        stage = torch.empty(mg.staging_bytes(r.W, r.H, world) // 4, dtype=torch.float32, device=f"cuda:{device}")
+        nbytes = mg.staging_bytes(r.W, r.H, world)
         plans = [mg.pack_plan(r.W, r.H, world, q) for q in range(world)]
-        host_staged = args.dist_backend == "gloo"
+        if args.dist_backend == "nccl" and not args.no_overlap:
+            # Pipelined: step k's staging buffer is gathered on RCCL's stream while step k+1
+            # renders on the kernel's stream; rank 0 unpacks step k into the final image
+            # after step k+1's frames are queued.  Two staging slots; every hand-off is a
+            # stream-side wait (no host sync), and the timed region ends with the last
+            # gather landed.
+            dev = torch.device("cuda", device)
+            ext = torch.cuda.ExternalStream(r.ctx.stream(), device=dev)
+            stages = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(2)]
+            parts = [[torch.empty_like(stages[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+            final = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16) if rank == 0 else None
+            pending = [None, None]
+            slot = [0]
 
-        def gather():
-            # pack this rank's bands (2-D device copy on the kernel's stream), gather the
-            # staging buffers to rank 0 over RCCL, unpack them into rank 0's image
-            mg.pack_device(r.ctx, r.out, plans[rank], stage.data_ptr())
-            r.finish()
-            parts = mg.gather_to_root(dist, stage.cpu() if host_staged else stage, rank, world)
-            if rank == 0:
-                if host_staged:
-                    parts = [p.to(stage.device) for p in parts]
-                torch.cuda.current_stream().synchronize()
-                for q in range(1, world):
-                    mg.unpack_device(r.ctx, parts[q].data_ptr(), plans[q], r.out)
+            def land(s):
+                if pending[s] is None:
+                    return
+                with torch.cuda.stream(ext):
+                    pending[s].wait()
+                if rank == 0:
+                    for q in range(world):
+                        mg.unpack_device(r.ctx, parts[s][q].data_ptr(), plans[q], final)
+                pending[s] = None
+
+            def gather():
+                s = slot[0]
+                slot[0] ^= 1
+                land(s ^ 1)
+                mg.pack_device(r.ctx, r.out, plans[rank], stages[s].data_ptr())
+                with torch.cuda.stream(ext):
+                    pending[s] = dist.gather(stages[s], parts[s], dst=0, async_op=True)
+
+            def land_all():
+                land(0)
+                land(1)
+        else:
+            stage = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{device}")
+            host_staged = args.dist_backend == "gloo"
+
+            def gather():
+                # pack this rank's bands (2-D device copy on the kernel's stream), gather the
+                # staging buffers to rank 0, unpack them into rank 0's image
+                mg.pack_device(r.ctx, r.out, plans[rank], stage.data_ptr())
                 r.finish()
+                parts = mg.gather_to_root(dist, stage.cpu() if host_staged else stage, rank, world)
+                if rank == 0:
+                    if host_staged:
+                        parts = [p.to(stage.device) for p in parts]
+                    torch.cuda.current_stream().synchronize()
+                    for q in range(1, world):
+                        mg.unpack_device(r.ctx, parts[q].data_ptr(), plans[q], r.out)
+                    r.finish()
 
         small_dev = f"cuda:{device}" if args.dist_backend == "nccl" else "cpu"
         tot = torch.tensor(counts, dtype=torch.float64, device=small_dev)
@@ -205,12 +249,18 @@ def main():
 
     def step():
         r.render()
-        r.finish()
         if gather is not None:
             gather()
+        else:
+            r.finish()
 
-    for _ in range(args.warmup):
-        step()
+    def steps(n):
+        for _ in range(n):
+            step()
+        if land_all is not None:
+            land_all()
+
+    steps(args.warmup)
 
     def sync_all():
         r.finish()
@@ -223,8 +273,7 @@ def main():
     r.k.reset_stats()
     sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    steps(args.steps)
     sync_all()
     elapsed = time.perf_counter() - t0
     ks = r.k.stats()
@@ -257,6 +306,17 @@ def main():
         except (ValueError, KeyError):
             traffic = None
 
+    if args.check_gather and final is not None:
+        # rank 0's own bands must have travelled out through RCCL and back into the final image
+        a = np.empty((r.H * r.W, 4), np.float32)
+        b = np.empty_like(a)
+        r.ctx.ReadBuffer(r.out, a)
+        r.ctx.ReadBuffer(final, b)
+        rows = np.concatenate([np.arange(bb * mg.BAND_ROWS, min(r.H, (bb + 1) * mg.BAND_ROWS)) for bb in r.bands])
+        a, b = a.reshape(r.H, r.W, 4)[rows], b.reshape(r.H, r.W, 4)[rows]
+        if not (a.view(np.uint32) == b.view(np.uint32)).all():
+            raise SystemExit("gathered image differs from the rendered bands")
+        print(f"check-gather: {rows.size} rows identical", file=sys.stderr)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -280,8 +340,9 @@ def main():
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
                    "math": args.math, "schedule": args.sched, "bvh": args.bvh, "parallelism": f"interleaved 8-row bands x{world}" + (
-                       (" + RCCL gather to rank 0" if args.dist_backend == "nccl" else " + gloo gather to rank 0 (host-staged)")
-                       if world > 1 else ""),
+                       (" + gloo gather to rank 0 (host-staged)" if args.dist_backend == "gloo" else
+                        " + RCCL gather to rank 0" + ("" if args.no_overlap else ", pipelined with the next step"))
+                       if dist is not None else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -1247,7 +1247,8 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                 a.hitT[sp.gid] = sh.t;
             }
             LaneStats sst;
-            const bool more = shade_bounce<M, kStats>(sh, sr, sp.radiance, sp.beta, sp.seed, sc, a, sst);
+            const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, sh, sr), sr, sp.radiance, sp.beta, sp.seed, sc,
+                                                      a, sst);
             if (kStats && mine) st.hits += sst.hits;
             ++sp.bounce;
             const bool cont = mine && more && sp.bounce < bounces;
@@ -1299,24 +1300,45 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                     u_nlanes += n_trav;
                 }
             }
+            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
+            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
             if (!leaf_step) {
-                if (state == kTrav) {
-                    if (kStats) ++st.visits;
-                    uint32_t next, first = 0, count = 0;
-                    if (node_visit<kLdsScene>(sc, a, cur, ray, h.t, next, first, count)) {
-                        state = kLeaf;
-                        leaf_i = first;
-                        leaf_end = first + count;
+#pragma unroll
+                for (int rep = 0; rep < kNodeBurst; ++rep) {
+                    if (state == kTrav) {
+                        if (kStats) ++st.visits;
+                        uint32_t next, first = 0, count = 0;
+                        if (kLdsScene) {
+                            uint32_t code;
+                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
+                                state = kLeaf;
+                                leaf_i = code;
+                            }
+                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
+                            state = kLeaf;
+                            leaf_i = first;
+                            leaf_end = first + count;
+                        }
+                        cur = next;
+                        if (state == kTrav && next == kEnd) state = kFin;
                     }
-                    cur = next;
-                    if (state == kTrav && next == kEnd) state = kFin;
                 }
             } else {
-                if (state == kLeaf) {
-                    if (kStats) ++st.tests;
-                    ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                    ++leaf_i;
-                    if (leaf_i == leaf_end) state = cur == kEnd ? kFin : kTrav;
+#pragma unroll
+                for (int rep = 0; rep < kTriBurst; ++rep) {
+                    if (state == kLeaf) {
+                        if (kStats) ++st.tests;
+                        if (kLdsScene) {
+                            const uint32_t idx = leaf_i & 0x00ffffffu;
+                            ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
+                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kFin : kTrav;
+                            leaf_i += 1u - (1u << 24);
+                        } else {
+                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                            ++leaf_i;
+                            if (leaf_i == leaf_end) state = cur == kEnd ? kFin : kTrav;
+                        }
+                    }
                 }
             }
         }

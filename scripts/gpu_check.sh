@@ -38,6 +38,8 @@ for step in "$@"; do
              run bench_dl_regen 600 python bench.py --math devicelib --sched regen --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     dist2) run dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --math devicelib ;;
+    dist1) run dist1_nccl_pipelined 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --force-dist --check-gather --steps 5 --warmup 1 --no-cpu-baseline && \
+           run dist1_nccl_sync 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29535 bench.py --force-dist --no-overlap --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchbunny) run bench_bunny 600 python bench.py --scene bunny --no-cpu-baseline --steps 3 ;;
     phase) run phase 300 python scripts/phase_profile.py ;;
     phasebunny) RT_PHASE_SCENE=bunny run phase_bunny 300 python scripts/phase_profile.py ;;
