@@ -98,8 +98,8 @@ struct SceneView {
     const float4* nodes;    // global path: 64-B node records (bounds, children, 8 skip pointers)
     const float4* tris;     // LDS or global
     const float4* onodes;   // LDS path: octant-resolved node records; global path: the LDS top
-    const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, -}, {n3, -}
-    const float4* smats;    // per material: {diffuse, roughness}, {specular, alpha}, {emission, 1/(alpha+1)}, {alpha^2/pi, alpha^2-1}
+    const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, n3.x}, {n3.yz, -, -}
+    const float4* smats;    // per material: {diffuse, 1/(alpha+1)}, {specular, alpha^2/pi}, {emission, alpha^2-1}, {roughness, alpha, -, -}
 };
 
 constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
@@ -231,8 +231,11 @@ struct TriEval {
 
 template <class M>
 __device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
-    const float4 a = tri[0], b = tri[1], c = tri[2];
-    const F3 p1{a.x, a.y, a.z}, e1{b.x, b.y, b.z}, e2{c.x, c.y, c.z};
+    // {p1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z}: two 16-B reads and one 4-B read (pack_tris)
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f a = *reinterpret_cast<const v4f*>(tri), b = *reinterpret_cast<const v4f*>(tri + 1);
+    const float c = *reinterpret_cast<const float*>(tri + 2);
+    const F3 p1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c};
     const F3 pvec = M::cross(r.d, e2);
     const float det = M::dot(e1, pvec);
     const float inv_det = 1.0f / det;
@@ -304,9 +307,9 @@ __device__ __forceinline__ void onb(F3 n, F3& s, F3& t) {
 struct MatView {
     F3 diffuse, specular, emission;
     // GGX constants of the material, formed once per material by pack_mats with the
-    // reference's operations (kernel_bvh.cl:229, :233, :283): alpha = 2/roughness^2 - 2,
+    // reference's operations (kernel_bvh.cl:229, :233, :283) from alpha = 2/roughness^2 - 2:
     // 1/(alpha + 1), alpha^2 * (1/pi), alpha^2 - 1
-    float alpha, inv_a1, a2pi, a2m1;
+    float inv_a1, a2pi, a2m1;
 };
 
 // SampleBrdf (kernel_bvh.cl:294-302) with SampleSpecular (:271-292) and SampleDiffuse
@@ -397,14 +400,19 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
     if (kStats) ++st.hits;
     // hit record of the last accepted triangle (kernel_bvh.cl:142-147), from the packed
     // shading records (bit copies of the normals, mtlIndex and material fields)
-    const float4 s1 = sc.stris[3 * h.prim], s2 = sc.stris[3 * h.prim + 1], s3 = sc.stris[3 * h.prim + 2];
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const float4* rec = sc.stris + 3 * h.prim;
+    const v4f s1 = *reinterpret_cast<const v4f*>(rec), s2 = *reinterpret_cast<const v4f*>(rec + 1);
+    const v2f s3 = *reinterpret_cast<const v2f*>(rec + 2);
     const float w = (1.0f - h.u) - h.v;
-    const F3 normal = normalize<M>((F3{s2.x, s2.y, s2.z} * h.u + F3{s3.x, s3.y, s3.z} * h.v) +
+    const F3 normal = normalize<M>((F3{s2.x, s2.y, s2.z} * h.u + F3{s2.w, s3.x, s3.y} * h.v) +
                                    F3{s1.x, s1.y, s1.z} * w);
     const F3 pos = ray.o + ray.d * h.t;
     const uint32_t mi = 4u * __float_as_uint(s1.w);
-    const float4 m0 = sc.smats[mi], m1 = sc.smats[mi + 1], m2 = sc.smats[mi + 2], m3 = sc.smats[mi + 3];
-    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m1.w, m2.w, m3.x, m3.y};
+    const v4f m0 = *reinterpret_cast<const v4f*>(sc.smats + mi), m1 = *reinterpret_cast<const v4f*>(sc.smats + mi + 1),
+              m2 = *reinterpret_cast<const v4f*>(sc.smats + mi + 2);
+    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m0.w, m1.w, m2.w};
 
     radiance = radiance + (beta * m.emission) * 50.0f;
     F3 wi = f3s(0.0f);
@@ -1392,8 +1400,8 @@ __global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __rest
     if (i >= n) return;
     const rt_cl_triangle& t = in[i];
     out[3 * i] = make_float4(t.v1.normal.x, t.v1.normal.y, t.v1.normal.z, __uint_as_float(t.mtlIndex));
-    out[3 * i + 1] = make_float4(t.v2.normal.x, t.v2.normal.y, t.v2.normal.z, 0.0f);
-    out[3 * i + 2] = make_float4(t.v3.normal.x, t.v3.normal.y, t.v3.normal.z, 0.0f);
+    out[3 * i + 1] = make_float4(t.v2.normal.x, t.v2.normal.y, t.v2.normal.z, t.v3.normal.x);
+    out[3 * i + 2] = make_float4(t.v3.normal.y, t.v3.normal.z, 0.0f, 0.0f);
 }
 
 __global__ void pack_mats(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
@@ -1402,10 +1410,11 @@ __global__ void pack_mats(const rt_cl_material* __restrict__ in, float4* __restr
     const rt_cl_material& m = in[i];
     const float alpha = 2.0f / (m.roughness * m.roughness) - 2.0f;  // pow(r, 2.0f) == r * r
     const float a2 = alpha * alpha;
-    out[4 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, m.roughness);
-    out[4 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, alpha);
-    out[4 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, 1.0f / (alpha + 1.0f));
-    out[4 * i + 3] = make_float4(a2 * kInvPi, a2 - 1.0f, 0.0f, 0.0f);
+    // the shading step reads the first three 16-B words whole; the fourth is informational
+    out[4 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, 1.0f / (alpha + 1.0f));
+    out[4 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, a2 * kInvPi);
+    out[4 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, a2 - 1.0f);
+    out[4 * i + 3] = make_float4(m.roughness, alpha, 0.0f, 0.0f);
 }
 
 __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
@@ -1413,9 +1422,11 @@ __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restr
     if (i >= n) return;
     const rt_float3 p1 = in[i].v1.position, p2 = in[i].v2.position, p3 = in[i].v3.position;
     // e1 = t2 - t1, e2 = t3 - t1 exactly as kernel_bvh.cl:109-110 computes them
-    out[3 * i] = make_float4(p1.x, p1.y, p1.z, 0.0f);
-    out[3 * i + 1] = make_float4(p2.x - p1.x, p2.y - p1.y, p2.z - p1.z, 0.0f);
-    out[3 * i + 2] = make_float4(p3.x - p1.x, p3.y - p1.y, p3.z - p1.z, 0.0f);
+    // 9 floats in a 48-B slot, packed so that a lane reads them with two 16-B and one 4-B
+    // access (3 x 12-B reads cost twice the LDS cycles of 3 x 16-B ones)
+    out[3 * i] = make_float4(p1.x, p1.y, p1.z, p2.x - p1.x);
+    out[3 * i + 1] = make_float4(p2.y - p1.y, p2.z - p1.z, p3.x - p1.x, p3.y - p1.y);
+    out[3 * i + 2] = make_float4(p3.z - p1.z, 0.0f, 0.0f, 0.0f);
 }
 
 }  // namespace rtk

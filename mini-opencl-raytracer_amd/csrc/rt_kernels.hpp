@@ -17,8 +17,8 @@ struct KernelArgs {
     const float4* packedTris;           // derived from slot 1: 3 x float4 per triangle
     const float4* octNodes;             // derived from slot 2: [node][octant] resolved records (LDS path)
     const float4* gNodes;               // derived from slot 2: 64-B node records (global path)
-    const float4* shadeTris;            // derived from slot 1: {n1, mtlIndex}, {n2}, {n3} per triangle
-    const float4* shadeMats;            // derived from slot 3: {diffuse, roughness}, {specular}, {emission}
+    const float4* shadeTris;            // derived from slot 1: {n1, mtlIndex}, {n2, n3.x}, {n3.yz} per triangle
+    const float4* shadeMats;            // derived from slot 3: {diffuse, 1/(a+1)}, {specular, a^2/pi}, {emission, a^2-1}, {rough, a}
     uint32_t nNodes, nTris, nMats;
     uint32_t nTop;                      // global path: leading gNodes records staged in LDS
     uint32_t width, height;             // slots 4, 5
