@@ -50,7 +50,10 @@ def parse():
     p.add_argument("--height", type=int, default=2160)
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--bounces", type=int, default=9)
-    p.add_argument("--math", choices=["pinned", "devicelib"], default="devicelib")
+    p.add_argument("--math", choices=["pinned", "devicelib", "shipped"], default="shipped",
+                   help="shipped (default): bit-exact with the reference as clBuildProgram builds it; "
+                        "devicelib: ... with -ffp-contract=off -cl-fp32-correctly-rounded-divide-sqrt; "
+                        "pinned: bit-exact with the CPU oracle")
     p.add_argument("--bvh", choices=["host", "device"], default="host",
                    help="host: the reference's SAH build (default); device: rtBuildBVH linear BVH")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
@@ -100,7 +103,7 @@ class Rank:
         k.set_float3(N.CAMERA_POS, CAMERA[0])
         k.set_float3(N.CAMERA_FRONT, CAMERA[1])
         k.set_float3(N.CAMERA_UP, CAMERA[2])
-        k.set_math_mode(N.MATH_DEVICELIB if args.math == "devicelib" else N.MATH_PINNED)
+        k.set_math_mode({"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[args.math])
         k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
                         "pool": N.SCHED_POOL}[args.sched])
         k.set_row_interleave(world, rank)

@@ -100,11 +100,18 @@ int rtFinish(rt_context ctx);
 int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset, size_t size,
                          const void* src);
 
-/* Math policy of the kernel: RT_MATH_PINNED (bit-identical to the pinned CPU
- * semantics of rt_pinned_math.h) or RT_MATH_DEVICELIB (default: the AMD OpenCL device-library
- * builtins the reference kernel gets on this GPU). */
+/* Math policy of the kernel:
+ *   RT_MATH_PINNED    -- bit-identical to the pinned CPU semantics of rt_pinned_math.h (oracle);
+ *   RT_MATH_DEVICELIB -- the AMD OpenCL device-library builtins the reference kernel
+ *                        gets on this GPU, contraction off, correctly rounded / and sqrt
+ *                        (the reference built -ffp-contract=off
+ *                        -cl-fp32-correctly-rounded-divide-sqrt);
+ *   RT_MATH_SHIPPED   -- default: the reference as clBuildProgram(" -I . ") builds it on this GPU
+ *                        (CLutils.cpp:52-66): devicelib builtins plus the compiler's default
+ *                        FP contraction and OpenCL C's 2.5-ulp division / 3-ulp sqrt. */
 #define RT_MATH_PINNED 0
 #define RT_MATH_DEVICELIB 1
+#define RT_MATH_SHIPPED 2
 int rtKernelSetMathMode(rt_kernel k, int mode);
 
 /* Work schedule of the kernel (same results, different lane scheduling):

@@ -69,7 +69,7 @@ LIGHT_BOUNCES, LIGHT_TYPE, SKYBOX_INTENSITY = 8, 9, 10
 CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
-MATH_PINNED, MATH_DEVICELIB = 0, 1
+MATH_PINNED, MATH_DEVICELIB, MATH_SHIPPED = 0, 1, 2
 SCHED_TILES, SCHED_REGEN, SCHED_STEP, SCHED_POOL = 0, 1, 2, 3
 
 

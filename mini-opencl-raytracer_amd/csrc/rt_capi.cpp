@@ -68,7 +68,7 @@ struct rt_kernel_s {
     rt_mem bufs[4] = {};
     uint32_t u32[RT_ARG_COUNT] = {};  // slots 4..10 (raw 4-byte values)
     float f3[3][4] = {};              // slots 11..13
-    int math = RT_MATH_DEVICELIB;
+    int math = RT_MATH_SHIPPED;  // the reference as its host builds it (rt_hip.h)
     int sched = RT_SCHED_STEP;
     uint32_t refill_min = 8, shade_min = 48;   // step schedule thresholds (swept on MI355X)
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
@@ -102,8 +102,8 @@ struct rt_kernel_s {
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[rtk::kNumSched][2][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
-    size_t occ_smem[rtk::kNumSched][2][2][2] = {};
+    int occ_cache[rtk::kNumSched][3][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
+    size_t occ_smem[rtk::kNumSched][3][2][2] = {};
 };
 
 namespace {
@@ -357,7 +357,8 @@ int prepare_scene(rt_kernel k) {
     }
     rc = ensure_dev(k->shade_tris, k->shade_tris_cap, (size_t)nt * 3);
     if (rc) return rc;
-    rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 4);
+    // two material tables: IEEE divisions (pinned, devicelib), then the shipped policy's
+    rc = ensure_dev(k->shade_mats, k->shade_mats_cap, (size_t)nmat * 8);
     if (rc) return rc;
     hipError_t e = rtk::launch_pack(static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
                                     k->shade_tris, static_cast<const rt_cl_material*>(mm->dptr), nmat,
@@ -602,7 +603,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.octNodes = k->oct_nodes;
     a.gNodes = k->g_nodes;
     a.shadeTris = k->shade_tris;
-    a.shadeMats = k->shade_mats;
+    a.shadeMats = k->shade_mats + (k->math == RT_MATH_SHIPPED ? 4 * (size_t)k->n_mats : 0);
     a.nMats = k->n_mats;
     a.nNodes = k->n_nodes;
     a.nTris = k->n_tris;
@@ -658,7 +659,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
                         (k->sched == RT_SCHED_STEP ? 4 * rtk::kFinishWaveBytes : 0);
     k->last_lds = lds;
 
-    const int mi = k->math == RT_MATH_DEVICELIB ? 1 : 0;
+    const int mi = k->math;
     const int si = k->sched;
     int& occ = k->occ_cache[si][mi][lds][k->stats];
     if (occ == 0 || k->occ_smem[si][mi][lds][k->stats] != smem) {
@@ -771,7 +772,7 @@ int rtFinish(rt_context ctx) {
 
 int rtKernelSetMathMode(rt_kernel k, int mode) {
     if (!k) return RT_INVALID_KERNEL;
-    if (mode != RT_MATH_PINNED && mode != RT_MATH_DEVICELIB) return RT_INVALID_VALUE;
+    if (mode != RT_MATH_PINNED && mode != RT_MATH_DEVICELIB && mode != RT_MATH_SHIPPED) return RT_INVALID_VALUE;
     k->math = mode;
     return RT_SUCCESS;
 }
@@ -919,7 +920,7 @@ int rtContextGetDevice(rt_context ctx, int* d) {
 }
 
 const char* rtGetBuildInfo(void) {
-    return "librt_hip: KernelEntry for gfx950 (HIP), math modes pinned|devicelib, scene in LDS or HBM";
+    return "librt_hip: KernelEntry for gfx950 (HIP), math modes pinned|devicelib|shipped, scene in LDS or HBM";
 }
 
 }  // extern "C"

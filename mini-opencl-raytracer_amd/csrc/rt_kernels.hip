@@ -1,959 +1,15 @@
-// rt_kernels.hip -- the hot path on gfx950: camera-ray generation, stack-based BVH
-// traversal, Moller-Trumbore triangle test, BRDF bounce loop and gamma accumulation.
-//
-// Replaces KernelEntry (/root/reference/kernel_bvh.cl:415-456) and everything it calls.
-// Written for CDNA4, not translated from the OpenCL source:
-//   * one ray per lane of a wave64; a 256-thread workgroup owns 16x16-pixel tiles
-//     (each wave an 8x8 sub-tile, so neighbouring rays share traversal paths) and walks
-//     them persistently (grid = resident workgroups), so the scene is staged into LDS
-//     once per workgroup, not once per tile;
-//   * BVH nodes are re-packed on the device into 32-byte records (two b128 LDS reads)
-//     and triangles into 48-byte {p1, e1 = p2-p1, e2 = p3-p1} records (three b128
-//     reads); both live in LDS when they fit (Cornell: 4.7 KB), else they are read from
-//     HBM/L2 through the same code (global path);
-//   * no traversal stack: the reference's stack walk (push the far child, pop on a miss
-//     or after a leaf) is a depth-first order whose child order depends only on the
-//     ray's octant, so it is replayed exactly with per-octant skip pointers (8 per
-//     node, built on the host): node visits, triangle tests and their order are the
-//     reference's, without LDS pushes/pops or the dependent pop latency;
-//   * traversal keeps only {t, primitive, u, v}; the hit record (position, shading
-//     normal, material) is formed once after the walk from the last accepted triangle,
-//     which yields the same values as the reference forming it at every accept;
-//   * no MFMA: this is branchy, latency-bound traversal.
-// Parity: every arithmetic step follows the reference's operation order with
-// -ffp-contract=off; transcendentals/dot/normalize come from the math policy
-// (rt_math.hpp).  Hit IDs are indices into the BVH-ordered triangle array, as
-// `isect.object - triangles` in the reference.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "../../include/rt_cl_types.h"
-#include "rt_kernels.hpp"
-#include "rt_math.hpp"
+// rt_kernels.hip -- KernelEntry entry points for the pinned and devicelib math policies,
+// the scene packing kernels and the host-side launch helpers.  The device code is
+// rt_kernels_body.hpp; the shipped policy lives in rt_kernels_shipped.hip.
+#include "rt_kernels_body.hpp"
 
 #pragma clang fp contract(off)
 
 namespace rtk {
 
-constexpr float kTwoPi = 6.28318530718f;    // kernel_bvh.cl:4
-constexpr float kInvPi = 0.31830988618f;    // kernel_bvh.cl:5
-constexpr float kMaxDist = 100000.0f;       // kernel_bvh.cl:7
-constexpr float kHitEps = 1.0e-8f;          // kernel_bvh.cl:101
-
-__device__ __forceinline__ F3 load3(const rt_float3& v) { return F3{v.x, v.y, v.z}; }
-
-// ---- RNG: kernel_bvh.cl:57-71 (integer, bit-exact by construction) ---------------------
-__device__ __forceinline__ uint32_t frame_hash(uint32_t x) { return 1103515245u * x + 12345u; }
-__device__ __forceinline__ float next_rand(uint32_t& s) {
-    uint32_t v = s;
-    v ^= v >> 16;
-    v *= 0x7feb352du;
-    v ^= v >> 15;
-    v *= 0x846ca68bu;
-    v ^= v >> 16;
-    s = v;
-    // float(v) / float(0xffffffff) == float(v) / 2^32, an exact power-of-two scaling
-    return (float)v * 0x1p-32f;
-}
-
-struct Ray {
-    F3 o, d, inv;
-    uint32_t sgn;  // bit i = invDir[i] < 0
-};
-
-// kernel_bvh.cl:42-55
-template <class M>
-__device__ __forceinline__ Ray init_ray(F3 o, F3 d) {
-    Ray r;
-    d = normalize<M>(d);
-    r.o = o;
-    r.d = d;
-    r.inv = F3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
-    return r;
-}
-
-// kernel_bvh.cl:386-403
-// (px, py) = (gid % W, gid / W), passed in by the callers that already know them.
-template <class M>
-__device__ __forceinline__ Ray create_ray(uint32_t px, uint32_t py, uint32_t W, uint32_t H, F3 pos, F3 front,
-                                          F3 up, float angle, uint32_t& seed) {
-    const float invW = 1.0f / (float)W;
-    const float invH = 1.0f / (float)H;
-    const float aspect = (float)W / (float)H;
-    float x = ((float)px + next_rand(seed)) - 0.5f;
-    float y = ((float)py + next_rand(seed)) - 0.5f;
-    x = ((2.0f * ((x + 0.5f) * invW) - 1.0f) * angle) * aspect;
-    y = -(1.0f - 2.0f * ((y + 0.5f) * invH)) * angle;
-    F3 dir = ((M::cross(front, up) * x) + (up * y)) + front;
-    return init_ray<M>(pos, normalize<M>(dir));
-}
-
-// ---- scene access ------------------------------------------------------------------------
-// Global (HBM/L2) scenes: packed node q0 = (bmin.x, bmin.y, bmin.z, bmax.x), q1 = (bmax.y,
-// bmax.z, offset, meta), meta = nPrimitives | axis << 16, plus [node][octant] skip pointers.
-// LDS scenes: octant-resolved records A[octant][node] = {near.xyz, far.x}, B[octant][node] =
-// {far.yz, hit_next, miss_next} (rt_capi.cpp, build_oct_nodes).  Packed triangle: p1, e1, e2 (w unused).
-struct SceneView {
-    const float4* nodes;    // global path: 64-B node records (bounds, children, 8 skip pointers)
-    const float4* tris;     // LDS or global
-    const float4* onodes;   // LDS path: octant-resolved node records; global path: the LDS top
-    const float4* stris;    // shading record per triangle: {n1, mtlIndex}, {n2, n3.x}, {n3.yz, -, -}
-    const float4* smats;    // per material: {diffuse, 1/(alpha+1)}, {specular, alpha^2/pi}, {emission, alpha^2-1}, {roughness, alpha, -, -}
-};
-
-constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
-constexpr uint32_t kLeafBit = 0x80000000u;  // octant record hit_next: leaf {first, count}
-
-// Scene into LDS once per workgroup (when it fits), else read in place.
-template <bool kLdsScene>
-__device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    if (kLdsScene) {
-        const int tid = threadIdx.x;
-        float4* lo = smem;
-        float4* lt = lo + 16 * a.nNodes;
-        float4* ls = lt + 3 * a.nTris;
-        float4* lm = ls + 3 * a.nTris;
-        for (uint32_t i = tid; i < 16 * a.nNodes; i += 256) lo[i] = a.octNodes[i];
-        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-        for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
-        for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
-        __syncthreads();
-        return SceneView{nullptr, lt, lo, ls, lm};
-    }
-    // global scene: the top-of-tree node records into LDS, the rest read from HBM/L2
-    const int tid = threadIdx.x;
-    for (uint32_t i = tid; i < 4 * a.nTop; i += 256) smem[i] = a.gNodes[i];
-    __syncthreads();
-    return SceneView{a.gNodes, a.packedTris, smem, a.shadeTris, a.shadeMats};
-}
-
-// LDS float4s of the scene (the finish queue / pool follow it)
-template <bool kLdsScene>
-__device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kLdsScene ? 16u * a.nNodes + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
-}
-
-struct Traversal {
-    float t;
-    int32_t prim;
-    float u, v;
-};
-
-// kernel_bvh.cl:156-169 (RayBounds).  max/min here only feed comparisons, where the
-// sign of a zero never matters and a NaN operand (0 * inf) must lose -- the fmax/fmin
-// hardware forms give the reference result in both math modes.
-__device__ __forceinline__ bool ray_bounds(const float4 q0, const float4 q1, const Ray& r,
-                                           float t) {
-    const float lox = q0.x, loy = q0.y, loz = q0.z, hix = q0.w, hiy = q1.x, hiz = q1.y;
-    const float nx = (r.sgn & 1u) ? hix : lox, fx = (r.sgn & 1u) ? lox : hix;
-    const float ny = (r.sgn & 2u) ? hiy : loy, fy = (r.sgn & 2u) ? loy : hiy;
-    const float nz = (r.sgn & 4u) ? hiz : loz, fz = (r.sgn & 4u) ? loz : hiz;
-    float t0 = __builtin_fmaxf(0.0f, (nx - r.o.x) * r.inv.x);
-    float t1 = __builtin_fminf(t, (fx - r.o.x) * r.inv.x);
-    t0 = __builtin_fmaxf(t0, (ny - r.o.y) * r.inv.y);
-    t1 = __builtin_fminf(t1, (fy - r.o.y) * r.inv.y);
-    t0 = __builtin_fmaxf(t0, (nz - r.o.z) * r.inv.z);
-    t1 = __builtin_fminf(t1, (fz - r.o.z) * r.inv.z);
-    return t1 >= t0;
-}
-
-// One node visit of kernel_bvh.cl:184-215: returns true when the ray enters a leaf (its
-// triangles [first, first + count) are tested next); `next` is the node the walk continues
-// at -- the near child of a passed interior node, else the octant's skip pointer.
-template <bool kOct>
-__device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
-                                           float t, uint32_t& next, uint32_t& first, uint32_t& count) {
-    if (kOct) {
-        const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
-        const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
-        float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
-        float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
-        t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
-        t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
-        t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
-        t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
-        const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
-        const bool hit = t1 >= t0;
-        const bool leaf = hit && (hn & kLeafBit);
-        next = (hit && !leaf) ? hn : mn;
-        first = hn & 0x00ffffffu;
-        count = ((hn >> 24) & 0x3fu) + 1u;
-        return leaf;
-    }
-    // global 64-B record; the first nTop records are read from their LDS copy (one flat load
-    // serves both address spaces)
-    const float4* nd = (cur < a.nTop ? sc.onodes : sc.nodes) + 4u * cur;
-    const float4 q0 = nd[0];
-    const float4 q1 = nd[1];
-    next = reinterpret_cast<const uint32_t*>(nd + 2)[r.sgn];
-    if (ray_bounds(q0, q1, r, t)) {
-        const uint32_t c0 = __float_as_uint(q1.z), c1 = __float_as_uint(q1.w);
-        const uint32_t axis = c1 >> 30;
-        if (axis == 3u) {
-            first = c0;
-            count = c1 & 0x3fffffffu;
-            return true;
-        }
-        next = ((r.sgn >> axis) & 1u) ? (c1 & 0x3fffffffu) : c0;
-    }
-    return false;
-}
-
-// LDS octant record visit returning the raw hit_next word on entering a leaf.
-__device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
-                                          float t, uint32_t& next, uint32_t& leaf_code) {
-    const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
-    const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
-    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
-    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
-    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
-    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
-    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
-    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
-    const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
-    const bool hit = t1 >= t0;
-    const bool leaf = hit && (hn & kLeafBit);
-    next = (hit && !leaf) ? hn : mn;
-    leaf_code = hn;
-    return leaf;
-}
-
-// kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
-// early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
-// ones the reference computes where it reaches them; the rest are discarded.  A wave
-// tests ~25 lanes' triangles at once and nearly always has some lane past every early
-// return, so the branches saved no arithmetic and cost exec-mask bookkeeping.
-struct TriEval {
-    float det, u, v, t;
-};
-
-template <class M>
-__device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
-    // {p1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z}: two 16-B reads and one 4-B read (pack_tris)
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f a = *reinterpret_cast<const v4f*>(tri), b = *reinterpret_cast<const v4f*>(tri + 1);
-    const float c = *reinterpret_cast<const float*>(tri + 2);
-    const F3 p1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c};
-    const F3 pvec = M::cross(r.d, e2);
-    const float det = M::dot(e1, pvec);
-    const float inv_det = 1.0f / det;
-    const F3 tvec = r.o - p1;
-    const float u = M::dot(tvec, pvec) * inv_det;
-    const F3 qvec = M::cross(tvec, e1);
-    const float v = M::dot(r.d, qvec) * inv_det;
-    const float t = M::dot(e2, qvec) * inv_det;
-    return TriEval{det, u, v, t};
-}
-
-// kUV = false: keep only {t, primitive} during the walk (two fewer live registers); the
-// barycentrics of the closest hit are re-evaluated at shading time (hit_uv) from the same
-// triangle and ray, which reproduces the accepted values bit for bit.
-template <class M, bool kUV = true>
-__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
-                                             Traversal& h) {
-    const TriEval e = tri_eval<M>(tri, r);
-    // (det < 1e-8 || -det > 1e-8) == det < 1e-8 (NaN falls through, as in the reference)
-    const bool ok = !(e.det < kHitEps) & !(e.u < 0.0f) & !(e.u > 1.0f) & !(e.v < 0.0f) &
-                    !(e.u + e.v > 1.0f) & (e.t < h.t);
-    if (ok) {
-        h.t = e.t;
-        h.prim = idx;
-        if (kUV) {
-            h.u = e.u;
-            h.v = e.v;
-        }
-    }
-}
-
-template <class M>
-__device__ __forceinline__ Traversal with_uv(const SceneView& sc, const Traversal& h, const Ray& r) {
-    const TriEval e = tri_eval<M>(sc.tris + 3 * (size_t)(h.prim < 0 ? 0 : h.prim), r);
-    return Traversal{h.t, h.prim, e.u, e.v};
-}
-
-// kernel_bvh.cl:171-219 (Intersect), replayed with the per-octant skip pointers: visiting
-// a node whose box is missed -- or finishing a leaf -- continues at skip[node][octant], the
-// node the reference pops next; a passed interior node continues at its near child
-// (the second child when sign[axis], kernel_bvh.cl:200-207).
-template <class M, bool kOct, bool kStats>
-__device__ __forceinline__ Traversal intersect(const SceneView& sc, const KernelArgs& a, const Ray& r,
-                                               uint32_t& visits, uint32_t& tests) {
-    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    uint32_t cur = 0;
-    while (cur != kEnd) {
-        if (kStats) ++visits;
-        uint32_t next, first = 0, count = 0;
-        if (node_visit<kOct>(sc, a, cur, r, h.t, next, first, count)) {
-            for (uint32_t i = 0; i < count; ++i) {
-                if (kStats) ++tests;
-                ray_triangle<M>(sc.tris + 3 * (size_t)(first + i), (int32_t)(first + i), r, h);
-            }
-        }
-        cur = next;
-    }
-    return h;
-}
-
-// ---- shading: kernel_bvh.cl:74-90, :221-347 ---------------------------------------------
-template <class M>
-__device__ __forceinline__ void onb(F3 n, F3& s, F3& t) {
-    const F3 axis = pm_fabs(n.x) > 0.001f ? F3{0.0f, 1.0f, 0.0f} : F3{1.0f, 0.0f, 0.0f};
-    t = normalize<M>(M::cross(axis, n));
-    s = M::cross(n, t);
-}
-
-struct MatView {
-    F3 diffuse, specular, emission;
-    // GGX constants of the material, formed once per material by pack_mats with the
-    // reference's operations (kernel_bvh.cl:229, :233, :283) from alpha = 2/roughness^2 - 2:
-    // 1/(alpha + 1), alpha^2 * (1/pi), alpha^2 - 1
-    float inv_a1, a2pi, a2m1;
-};
-
-// SampleBrdf (kernel_bvh.cl:294-302) with SampleSpecular (:271-292) and SampleDiffuse
-// (:264-269).  G and F of SampleSpecular are dead in the reference and not evaluated.
-//
-// SampleGGX (:227-239) and SampleHemisphereCosine (:79-90) end in the same expression,
-// normalize((s*cos(phi))*sinT + (t*sin(phi))*sinT + n*c), with c = cosTheta (GGX) or
-// sqrt(1 - sinThetaSqr) (cosine).  The lane-specific scalars are drawn in a short branch
-// and the expensive tail (frame, sin, cos, normalize) is executed once for both kinds of
-// lanes -- each lane still performs exactly the reference's operations, in its order.
-template <class M>
-__device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const MatView& m,
-                                          uint32_t& seed) {
-    const bool spec = next_rand(seed) > 0.5f;
-    const float phi = kTwoPi * next_rand(seed);
-    float sinT, c;
-    if (spec) {
-        (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
-        const float r = next_rand(seed);
-        c = M::pow(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
-        sinT = __builtin_sqrtf(M::max(0.0f, 1.0f - c * c));
-    } else {
-        const float s2 = next_rand(seed);
-        sinT = __builtin_sqrtf(s2);
-        c = __builtin_sqrtf(1.0f - s2);
-    }
-    F3 s, t;
-    onb<M>(n, s, t);
-    float sphi, cphi;
-    M::sincos(phi, sphi, cphi);
-    const F3 pa = (s * cphi) * sinT;
-    const F3 pb = (t * sphi) * sinT;
-    const F3 dir = normalize<M>((pa + pb) + n * c);
-    if (spec) {
-        const F3 wh = dir;
-        const float cosTheta = c;
-        wi = (-wo) + wh * (2.0f * M::dot(wo, wh));
-        if (M::dot(wi, n) * M::dot(wo, n) < 0.000001f) return f3s(0.0f);
-        const float D = m.a2pi / M::pow2(cosTheta * cosTheta * m.a2m1 + 1.0f);
-        pdf = (D * cosTheta) / (4.0f * M::max(M::dot(wo, wh), 0.0f));
-        const float denom =
-            (4.0f * M::max(M::dot(wi, n), 0.0f)) * M::max(M::dot(wo, n), 0.0f) + 0.001f;
-        return m.specular * (D / denom);
-    }
-    wi = dir;
-    pdf = M::dot(wi, n) * kInvPi;
-    return m.diffuse * kInvPi;
-}
-
-// kernel_bvh.cl:304-347
-template <class M>
-__device__ __forceinline__ float light_pixel(const Ray& r, float t, F3 normal, int lightType) {
-    const F3 lightPosition{0.0f, -10.0f, 16.0f};
-    const F3 lightDirection{-0.5f, 0.4f, -0.1f};
-    float intensity = 1.0f, NdotL, attn = 1.0f;
-    if (lightType <= 0) {
-        NdotL = M::max(M::dot(normal, -lightDirection), 0.0f);
-    } else {
-        const F3 X = r.o + r.d * t;
-        const F3 L = lightPosition - X;
-        NdotL = M::max(M::dot(normal, L), 0.0f);
-        if (lightType == 1) {
-            intensity = 16.0f;
-            const float falloff = 0.8f;
-            const F3 eye = L - X;
-            const float d = __builtin_sqrtf(M::dot(eye, eye));
-            attn = (float)(1.0 / (double)(falloff * (d * d)));  // `1.0` is a double literal
-        }
-    }
-    return (attn * intensity) * NdotL;
-}
-
-struct LaneStats {
-    uint32_t rays = 0, visits = 0, tests = 0, hits = 0;
-};
-
-// The body of Render's bounce loop after Intersect (kernel_bvh.cl:358-380): radiance and
-// beta updates, BRDF sample and the next ray.  Returns false where the reference breaks
-// out of the loop (miss, or pdf <= 0 / NaN).
-template <class M, bool kStats>
-__device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& radiance, F3& beta,
-                                             uint32_t& seed, const SceneView& sc, const KernelArgs& a,
-                                             LaneStats& st) {
-    if (h.prim < 0) {
-        radiance = radiance + beta * f3s(0.5f * a.skyboxIntensity);
-        return false;
-    }
-    if (kStats) ++st.hits;
-    // hit record of the last accepted triangle (kernel_bvh.cl:142-147), from the packed
-    // shading records (bit copies of the normals, mtlIndex and material fields)
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    typedef float v2f __attribute__((ext_vector_type(2)));
-    const float4* rec = sc.stris + 3 * h.prim;
-    const v4f s1 = *reinterpret_cast<const v4f*>(rec), s2 = *reinterpret_cast<const v4f*>(rec + 1);
-    const v2f s3 = *reinterpret_cast<const v2f*>(rec + 2);
-    const float w = (1.0f - h.u) - h.v;
-    const F3 normal = normalize<M>((F3{s2.x, s2.y, s2.z} * h.u + F3{s2.w, s3.x, s3.y} * h.v) +
-                                   F3{s1.x, s1.y, s1.z} * w);
-    const F3 pos = ray.o + ray.d * h.t;
-    const uint32_t mi = 4u * __float_as_uint(s1.w);
-    const v4f m0 = *reinterpret_cast<const v4f*>(sc.smats + mi), m1 = *reinterpret_cast<const v4f*>(sc.smats + mi + 1),
-              m2 = *reinterpret_cast<const v4f*>(sc.smats + mi + 2);
-    MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m0.w, m1.w, m2.w};
-
-    radiance = radiance + (beta * m.emission) * 50.0f;
-    F3 wi = f3s(0.0f);
-    float pdf = 0.0f;
-    const F3 f = sample_brdf<M>(-ray.d, wi, pdf, normal, m, seed);
-    if (pdf <= 0.0f || pdf != pdf) return false;
-    const F3 mul = (f * M::dot(wi, normal)) / pdf;
-    beta = beta * mul;
-    const float lp = light_pixel<M>(ray, h.t, normal, a.lightType);
-    radiance = radiance + (f3s(lp) * m.diffuse) * beta;
-    ray = init_ray<M>(pos + wi * 0.01f, wi);
-    return true;
-}
-
-// kernel_bvh.cl:349-384 (Render)
-template <class M, bool kOct, bool kStats>
-__device__ __forceinline__ F3 render(const SceneView& sc, Ray ray,
-                                     uint32_t& seed, const KernelArgs& a,
-                                     int32_t& prim_id, float& prim_t, LaneStats& st) {
-    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    for (uint32_t i = 0; i < bounces; ++i) {
-        if (kStats) ++st.rays;
-        const Traversal h = intersect<M, kOct, kStats>(sc, a, ray, st.visits, st.tests);
-        if (i == 0) {
-            prim_id = h.prim;
-            prim_t = h.t;
-        }
-        if (!shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st)) break;
-    }
-    return F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
-}
-
-// kernel_bvh.cl:449-455: write (frameCount 0) or gamma-accumulate one work-item's result.
-template <class M>
-__device__ __forceinline__ void finish_color(const KernelArgs& a, uint32_t gid, F3 rad) {
-    F3 out;
-    if (a.frameCount == 0) {
-        out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
-    } else {
-        const float4 old = a.result[gid];
-        const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
-        const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
-        const F3 acc = ((lin * fm1) + rad) / fc;
-        out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
-    }
-    a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
-}
-
-template <class M>
-__device__ __forceinline__ void finish_pixel(const KernelArgs& a, uint32_t gid, F3 rad, int32_t pid,
-                                             float pt) {
-    finish_color<M>(a, gid, rad);
-    if (a.hitIds) {
-        a.hitIds[gid] = pid;
-        a.hitT[gid] = pt;
-    }
-}
-
-__device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
-    unsigned long long x = v;
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-}
-
-__device__ __forceinline__ void flush_stats(const KernelArgs& a, const LaneStats& st, int lane) {
-    const unsigned long long r = wave_sum(st.rays), v = wave_sum(st.visits), t = wave_sum(st.tests),
-                             h = wave_sum(st.hits);
-    if (lane == 0) {
-        atomicAdd(&a.stats[0], r);
-        atomicAdd(&a.stats[1], v);
-        atomicAdd(&a.stats[2], t);
-        atomicAdd(&a.stats[3], h);
-    }
-}
-
-// ---- the kernel (tile schedule) ------------------------------------------------------------
-template <class M, bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    // tan(0.5f * (45.0f * 3.1415f / 180.0f)), kernel_bvh.cl:392
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));
-    const uint32_t fh = frame_hash(a.frameCount);
-
-    const int wave = tid >> 6, lane = tid & 63;
-    const uint32_t dx = (uint32_t)((wave & 1) * 8 + (lane & 7));
-    const uint32_t dy = (uint32_t)((wave >> 1) * 8 + (lane >> 3));
-
-    LaneStats st;
-    for (uint32_t tile = blockIdx.x; tile < a.nTiles; tile += gridDim.x) {
-        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-        const uint32_t x = tx * 16 + dx;
-        const uint32_t row = a.rowBegin + ty * 16 + dy;
-        const uint64_t g64 = (uint64_t)row * a.width + x;
-        if (x >= a.width || g64 < a.gidBegin || g64 >= a.gidEnd) continue;
-        const uint32_t gid = (uint32_t)g64;
-
-        uint32_t seed = gid + fh;  // kernel_bvh.cl:445
-        const Ray ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
-        int32_t pid = -1;
-        float pt = 0.0f;
-        const F3 rad = render<M, kLdsScene, kStats>(sc, ray, seed, a, pid, pt, st);
-        finish_pixel<M>(a, gid, rad, pid, pt);
-    }
-    if (kStats) flush_stats(a, st, lane);
-}
-
-// Work distribution of the persistent schedules (guided self-scheduling): pixels are handed
-// out in chunks of whole 8x8 tiles from two global counters -- chunks of a.chunkPixels over the
-// first a.chunkSplit pixels, then chunks of a.tailChunk.  Large chunks keep the returning
-// atomics per frame low (one counter saturates near 90 per microsecond on MI355X); small
-// ones at the end keep the last waves from finishing alone.  Returns false when no work is left.
-__device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
-                                           uint32_t& len, bool& tail) {
-    uint32_t b = 0;
-    if (!tail) {
-        if (lane == 0) b = atomicAdd(&a.workCounter[0], a.chunkPixels);
-        b = __shfl(b, 0, 64);
-        if (b < a.chunkSplit) {
-            base = b;
-            len = min(a.chunkPixels, a.chunkSplit - b);
-            return true;
-        }
-        tail = true;  // this wave never asks the bulk counter again
-    }
-    if (lane == 0) b = atomicAdd(&a.workCounter[1], a.tailChunk);
-    b = __shfl(b, 0, 64) + a.chunkSplit;
-    if (b >= total) return false;
-    base = b;
-    len = min(a.tailChunk, total - b);
-    return true;
-}
-
-// ---- path-regeneration schedule -------------------------------------------------------------
-// Same per-pixel computation, different scheduling: every lane of a persistent wave carries
-// one path; when a path ends (miss, pdf break, or lightBounces reached) the lane writes its
-// pixel and immediately starts the next pixel, taken from the wave's current 64-pixel chunk
-// (one 8x8 tile; one global atomic per chunk).  Lanes therefore stay busy across bounces
-// instead of idling until the longest path of their tile ends.  Every pixel still runs the
-// reference's exact sequence of operations with its own seed, so results are identical.
-template <class M, bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;  // index space: 8x8-pixel tiles, tile-major
-    const uint32_t rowEnd = a.rowBegin + a.rowCount;
-    const int lane = tid & 63;
-
-    LaneStats st;
-    bool active = false;
-    uint32_t gid = 0, seed = 0, bounce = 0;
-    int32_t pid = -1;
-    float pt = 0.0f;
-    Ray ray{};
-    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
-    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
-    // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
-    bool exhausted = false;                    // wave-uniform
-
-    for (;;) {
-        // ---- refill idle lanes from the wave's chunk --------------------------------------
-        while (!exhausted) {
-            const unsigned long long idle = __ballot(!active);
-            if (idle == 0ull) break;
-            if (chunk_used >= chunk_len) {
-                if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                    exhausted = true;
-                    break;
-                }
-                chunk_used = 0;
-            }
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
-            if (!active && rank < take) {
-                const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                const uint32_t x = tx * 8u + (w & 7u),
-                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
-                const uint64_t g64 = (uint64_t)row * a.width + x;
-                if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
-                    gid = (uint32_t)g64;
-                    seed = gid + fh;  // kernel_bvh.cl:445
-                    ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
-                    radiance = f3s(0.0f);
-                    beta = f3s(1.0f);
-                    bounce = 0;
-                    pid = -1;
-                    pt = 0.0f;
-                    if (bounces > 0u) {
-                        active = true;
-                    } else {
-                        finish_pixel<M>(a, gid, f3s(0.0f), pid, pt);  // no bounce: radiance 0
-                    }
-                }
-            }
-            chunk_used += take;
-        }
-        if (__ballot(active) == 0ull) {
-            if (exhausted) break;
-            continue;
-        }
-        // ---- one bounce of every live path -------------------------------------------------
-        if (active) {
-            if (kStats) ++st.rays;
-            const Traversal h = intersect<M, kLdsScene, kStats>(sc, a, ray, st.visits, st.tests);
-            if (bounce == 0u) {
-                pid = h.prim;
-                pt = h.t;
-            }
-            bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
-            ++bounce;
-            if (!more || bounce >= bounces) {
-                const F3 rad{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
-                finish_pixel<M>(a, gid, rad, pid, pt);
-                active = false;
-            }
-        }
-    }
-    if (kStats) flush_stats(a, st, lane);
-}
-
-// ---- step schedule: a per-wave state machine ------------------------------------------------
-// Every lane is in one of four states:
-//   IDLE  -- no path; refilled (new pixel -> camera ray) when enough lanes are idle
-//   TRAV  -- at BVH node `cur`: one RayBounds per step (kernel_bvh.cl:184-215)
-//   LEAF  -- inside a passing leaf: ONE RayTriangle per step, in the leaf's order
-//   SHADE -- traversal finished; shaded when enough lanes are ready (kernel_bvh.cl:358-380)
-//   DONE  -- path finished; its pixel is accumulated (kernel_bvh.cl:449-455) together with
-//            the refill, so that code also runs with many lanes
-// Each step advances every TRAV/LEAF lane by one node or one triangle, so a wave no longer
-// runs a 4-triangle leaf loop for the few lanes that happen to sit at a leaf, and the heavy
-// per-bounce (shading) and per-path (accumulate + next camera ray) code runs with many lanes
-// at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
-// t, hit and pixel -- is exactly the reference's.
-constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
-
-__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// Finish queue: the gamma accumulation (kernel_bvh.cl:449-455, six pow per pixel) of
-// finished paths runs 64 pixels at a time instead of with the few lanes whose paths
-// happen to end in a refill round.  Pixels are independent and each is written once per
-// launch, so the order of finishing does not matter.
-constexpr uint32_t kFinishSlots = 64;
-static_assert(kFinishWaveBytes == kFinishSlots * 16, "finish queue layout");
-
-template <class M>
-__device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4* fq, uint32_t n, uint32_t lane) {
-    if (lane < n) {
-        const float4 e = fq[lane];
-        finish_color<M>(a, __float_as_uint(e.w), F3{e.x, e.y, e.z});
-    }
-}
-// steps of the chosen kind per scheduling decision (thresholds are re-checked after each
-// burst): the per-step ballots and threshold tests cost about as much as a node visit
-#ifndef RT_NODE_BURST
-#define RT_NODE_BURST 6
-#endif
-#ifndef RT_TRI_BURST
-#define RT_TRI_BURST 2
-#endif
-// the same for scenes read from HBM/L2 (global path)
-#ifndef RT_GNODE_BURST
-#define RT_GNODE_BURST RT_NODE_BURST
-#endif
-#ifndef RT_GTRI_BURST
-#define RT_GTRI_BURST RT_TRI_BURST
-#endif
-
-
-__device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
-
-template <class M, bool kLdsScene, bool kStats>
-__device__ __forceinline__ void step_body(const KernelArgs& a) {
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;
-    const uint32_t rowEnd = a.rowBegin + a.rowCount;
-    const int lane = tid & 63;
-    const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
-    const uint32_t kShadeMin = a.shadeMin;    // shade when this many lanes are ready
-
-    // per-wave finish queue in LDS (after the scene): {radiance, gid} of finished paths
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    float4* fq = smem + lds_scene_f4<kLdsScene>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
-    uint32_t fq_n = 0;  // wave-uniform
-
-    LaneStats st;
-    uint32_t state = kIdle;
-    uint32_t gid = 0, seed = 0, bounce = 0;
-    Ray ray{};
-    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
-    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    uint32_t cur = 0;  // TRAV: node to visit; LEAF: node to continue at after the leaf
-    uint32_t leaf_i = 0, leaf_end = 0;
-    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
-    // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
-    bool exhausted = false;                    // wave-uniform
-    // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
-    uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
-    const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
-    // diagnostic lane-utilisation counters (wave-uniform): steps / rounds and lanes served
-    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
-             u_rrounds = 0, u_rlanes = 0, u_other = 0, u_shadew = 0, u_freew = 0, u_pad = 0;
-
-    for (;;) {
-        // ---- finish + refill: accumulate finished paths, start new pixels ----------------------
-        uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        const uint32_t n_free = popc_ballot(state == kIdle || state == kDone);
-        if (n_free == 64u || (!exhausted && n_free >= kRefillMin)) {
-            if (kStats) {
-                ++u_rrounds;
-                u_rlanes += n_free;
-            }
-            // finished paths: hit outputs now, the gamma accumulation through the finish queue
-            const unsigned long long done = __ballot(state == kDone);
-            if (done != 0ull) {
-                const uint32_t nd = (uint32_t)__popcll(done);
-                const uint32_t rank = lane_rank(done);
-                const uint32_t fit = kFinishSlots - fq_n;
-                if (state == kDone) {
-                    if (rank < fit) fq[fq_n + rank] = make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(gid));
-                }
-                if (nd >= fit) {
-                    finish_queued<M>(a, fq, kFinishSlots, lane);
-                    if (state == kDone && rank >= fit)
-                        fq[rank - fit] = make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(gid));
-                    fq_n = nd - fit;
-                } else {
-                    fq_n += nd;
-                }
-                if (state == kDone) state = kIdle;
-            }
-            while (!exhausted) {
-                const unsigned long long idle = __ballot(state == kIdle);
-                if (idle == 0ull) break;
-                if (chunk_used >= chunk_len) {
-                    if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                        exhausted = true;
-                        break;
-                    }
-                    chunk_used = 0;
-                }
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
-                if (state == kIdle && rank < take) {
-                    const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                    const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                    const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                    const uint32_t x = tx * 8u + (w & 7u),
-                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
-                    const uint64_t g64 = (uint64_t)row * a.width + x;
-                    if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
-                        gid = (uint32_t)g64;
-                        seed = gid + fh;  // kernel_bvh.cl:445
-                        ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
-                        radiance = f3s(0.0f);
-                        beta = f3s(1.0f);
-                        bounce = 0;
-                        if (bounces > 0u) {
-                            state = kTrav;
-                            h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                            cur = 0;
-                            if (kStats) ++st.rays;
-                        } else {
-                            state = kDone;  // no bounce: radiance max(0, 0) = 0
-                            if (a.hitIds) {
-                                a.hitIds[gid] = -1;
-                                a.hitT[gid] = 0.0f;
-                            }
-                        }
-                    }
-                }
-                chunk_used += take;
-            }
-        }
-        uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats) cyc_refill += tB - tA;
-        {
-            const uint32_t n_idle = popc_ballot(state == kIdle);
-            if (n_idle == 64u) {
-                if (exhausted) break;
-                continue;
-            }
-        }
-
-        // ---- traversal steps -----------------------------------------------------------------
-        // Each step is wave-uniform: either a node step (TRAV lanes visit one node) or a
-        // triangle step (LEAF lanes test one triangle), chosen by which serves more lanes per
-        // instruction (weights ~ the two bodies' VALU cost), so the wave never pays both
-        // bodies for a mix of lanes.
-        for (;;) {
-            const uint32_t n_trav = popc_ballot(state == kTrav);
-            const uint32_t n_leaf = popc_ballot(state == kLeaf);
-            if (n_trav + n_leaf == 0u) break;
-            if (popc_ballot(state == kShade) >= kShadeMin) break;
-            if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
-            const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
-            if (kStats) {
-                u_shadew += popc_ballot(state == kShade);
-                u_freew += popc_ballot(state == kIdle || state == kDone);
-                u_other += leaf_step ? n_trav : n_leaf;
-                if (leaf_step) {
-                    ++u_tsteps;
-                    u_tlanes += n_leaf;
-                } else {
-                    ++u_nsteps;
-                    u_nlanes += n_trav;
-                }
-            }
-            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
-            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
-            if (!leaf_step) {
-#pragma unroll
-                for (int rep = 0; rep < kNodeBurst; ++rep) {
-                    if (state == kTrav) {
-                        if (kStats) ++st.visits;
-                        uint32_t next, first = 0, count = 0;
-                        if (kLdsScene) {
-                            // LDS records: the LEAF state keeps the packed leaf word itself
-                            // (bit 31 | count-1 << 24 | first); the triangle steps walk it
-                            uint32_t code;
-                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
-                                state = kLeaf;
-                                leaf_i = code;
-                            }
-                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
-                            state = kLeaf;
-                            leaf_i = first;
-                            leaf_end = first + count;
-                        }
-                        cur = next;
-                        if (state == kTrav && next == kEnd) state = kShade;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int rep = 0; rep < kTriBurst; ++rep) {
-                    if (state == kLeaf) {
-                        if (kStats) ++st.tests;
-                        if (kLdsScene) {
-                            const uint32_t idx = leaf_i & 0x00ffffffu;
-                            ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kShade : kTrav;
-                            leaf_i += 1u - (1u << 24);
-                        } else {
-                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                            ++leaf_i;
-                            if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
-                        }
-                    }
-                }
-            }
-        }
-
-        // ---- shading ---------------------------------------------------------------------------
-        uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats) {
-            cyc_trav += tC - tB;
-            const uint32_t ns = popc_ballot(state == kShade);
-            if (ns) {
-                ++u_srounds;
-                u_slanes += ns;
-            }
-        }
-        if (state == kShade) {
-            if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension)
-                a.hitIds[gid] = h.prim;
-                a.hitT[gid] = h.t;
-            }
-            const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, h, ray), ray, radiance, beta, seed, sc, a, st);
-            ++bounce;
-            if (!more || bounce >= bounces) {
-                radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
-                state = kDone;
-            } else {
-                state = kTrav;
-                h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                cur = 0;
-                if (kStats) ++st.rays;
-            }
-        }
-        if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tC;
-    }
-    finish_queued<M>(a, fq, fq_n, lane);
-    if (kStats) {
-        flush_stats(a, st, lane);
-        if (lane == 0) {
-            atomicAdd(&a.stats[4], (unsigned long long)cyc_refill);
-            atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
-            atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
-            atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
-            atomicAdd(&a.stats[8], (unsigned long long)u_nsteps);
-            atomicAdd(&a.stats[9], (unsigned long long)u_nlanes);
-            atomicAdd(&a.stats[10], (unsigned long long)u_tsteps);
-            atomicAdd(&a.stats[11], (unsigned long long)u_tlanes);
-            atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
-            atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
-            atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
-            atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
-            atomicAdd(&a.stats[16], (unsigned long long)u_other);
-            atomicAdd(&a.stats[17], (unsigned long long)u_shadew);
-            atomicAdd(&a.stats[18], (unsigned long long)u_freew);
-            atomicAdd(&a.stats[19], (unsigned long long)u_pad);
-        }
-    }
-}
-
 // Entry points per math policy: the devicelib body fits 80 VGPRs with a small spill, and
 // 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
 // (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
-#ifndef RT_STEP_DEVICELIB_WAVES
-#define RT_STEP_DEVICELIB_WAVES 5
-#endif
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
 void kernel_entry_step_devicelib(KernelArgs a) {
@@ -967,412 +23,6 @@ void kernel_entry_step_devicelib(KernelArgs a) {
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
     step_body<MathPinned, kLdsScene, kStats>(a);
-}
-
-// ---- pool schedule: per-wave LDS path pool, full-wave shading ------------------------------
-// The step schedule leaves a third of a wave idle during traversal at 9 bounces: lanes whose
-// traversal ended wait (up to the shading threshold) and freed lanes wait for a refill
-// batch (profiles/r01/phase_*.txt).  Here every wave owns a pool of 64 path records in LDS
-// (the "hit" or "continuation" of a path, 112 B slots) and three slot stacks:
-//   trace-ready -- a continuation ray produced by shading, waiting for a lane
-//   shade-ready -- a finished traversal (ray + {t, primitive, u, v}) waiting for shading
-//   free
-// A lane whose traversal ends parks its path as shade-ready -- exchanging it for a
-// continuation when one is waiting -- and keeps tracing; idle lanes take continuations, then
-// new camera rays.  Shading runs when 64 records are ready (a full wave), each lane
-// shading one record in registers separate from its own traversal state, and writes the
-// continuation back into the same slot (or accumulates the pixel when the path ends).
-// Per path the operations, their order and the RNG stream are the reference's, so every
-// pixel and hit is bit-identical to the other schedules.  No cross-wave communication:
-// the pool is wave-private, LDS ops of one wave execute in order, no barriers.
-constexpr uint32_t kFin = 3;  // pool schedule: traversal finished, waiting to be parked
-constexpr uint32_t kPoolSlots = 64;
-constexpr uint32_t kPoolChunks = 7;
-static_assert(kPoolWaveBytes == kPoolSlots * kPoolChunks * 16 + 3 * kPoolSlots * 4, "pool layout");
-
-struct PoolView {
-    float4* rec;       // [chunk][slot] float4
-    uint32_t* tstack;  // trace-ready slots
-    uint32_t* sstack;  // shade-ready slots
-    uint32_t* fstack;  // free slots
-};
-
-struct PathState {
-    uint32_t gid, seed, bounce;
-    F3 radiance, beta;
-};
-
-// shade-ready record: o, d, {t, prim, u, v}, path state
-__device__ __forceinline__ void pool_put_hit(const PoolView& p, uint32_t s, const Ray& r, const Traversal& h,
-                                             const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, h.t, __int_as_float(h.prim));
-    p.rec[2 * kPoolSlots + s] = make_float4(h.u, h.v, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
-    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
-    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_hit(const PoolView& p, uint32_t s, Ray& r, Traversal& h, PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    h = Traversal{c1.z, __float_as_int(c1.w), c2.x, c2.y};
-    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
-                   F3{c4.x, c4.y, c4.z}};
-}
-
-// trace-ready record: the initialised next ray (o, d, 1/d) and path state
-__device__ __forceinline__ void pool_put_ray(const PoolView& p, uint32_t s, const Ray& r, const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
-    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, 0.0f, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
-    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
-    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_ray(const PoolView& p, uint32_t s, Ray& r, PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    r.inv = F3{c1.z, c1.w, c2.x};
-    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
-    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
-                   F3{c4.x, c4.y, c4.z}};
-}
-
-// a lane's in-flight state (any lane state), parked in a slot during a shading round
-__device__ __forceinline__ void pool_put_lane(const PoolView& p, uint32_t s, uint32_t state, const Ray& r,
-                                              const Traversal& h, uint32_t cur, uint32_t leaf_i,
-                                              uint32_t leaf_end, const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
-    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, h.t, __int_as_float(h.prim), h.u);
-    p.rec[3 * kPoolSlots + s] = make_float4(h.v, __uint_as_float(cur), __uint_as_float(leaf_i),
-                                            __uint_as_float(leaf_end));
-    p.rec[4 * kPoolSlots + s] = make_float4(__uint_as_float(state), __uint_as_float(ps.gid),
-                                            __uint_as_float(ps.seed), __uint_as_float(ps.bounce));
-    p.rec[5 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, ps.beta.x);
-    p.rec[6 * kPoolSlots + s] = make_float4(ps.beta.y, ps.beta.z, 0.0f, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_lane(const PoolView& p, uint32_t s, uint32_t& state, Ray& r,
-                                              Traversal& h, uint32_t& cur, uint32_t& leaf_i, uint32_t& leaf_end,
-                                              PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s], c5 = p.rec[5 * kPoolSlots + s],
-                 c6 = p.rec[6 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    r.inv = F3{c1.z, c1.w, c2.x};
-    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
-    h = Traversal{c2.y, __float_as_int(c2.z), c2.w, c3.x};
-    cur = __float_as_uint(c3.y);
-    leaf_i = __float_as_uint(c3.z);
-    leaf_end = __float_as_uint(c3.w);
-    state = __float_as_uint(c4.x);
-    ps = PathState{__float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w), F3{c5.x, c5.y, c5.z},
-                   F3{c5.w, c6.x, c6.y}};
-}
-
-template <class M, bool kLdsScene, bool kStats>
-__device__ __forceinline__ void pool_body(const KernelArgs& a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-    const uint32_t scene_f4 = lds_scene_f4<kLdsScene>(a);
-    float4* region = smem + scene_f4 + (uint32_t)(tid >> 6) * (kPoolWaveBytes / 16u);
-    uint32_t* stacks = reinterpret_cast<uint32_t*>(region + kPoolChunks * kPoolSlots);
-    const PoolView pv{region, stacks, stacks + kPoolSlots, stacks + 2 * kPoolSlots};
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;
-    const uint32_t rowEnd = a.rowBegin + a.rowCount;
-    const uint32_t lane = (uint32_t)(tid & 63);
-    const uint32_t kRefillMin = a.refillMin;  // camera rays when this many lanes are idle
-    const uint32_t kShadeMin = a.poolShadeMin;  // shade when this many records are ready
-    const uint32_t kParkMin = a.parkMin;      // park when this many traversals have ended
-    const uint32_t kLowWork = a.lowWork;      // ... or shade early when tracing work runs low
-
-    pv.fstack[lane] = lane;
-    uint32_t nt = 0, ns = 0, ne = kPoolSlots;  // stack depths (wave-uniform)
-
-    LaneStats st;
-    uint32_t state = kIdle;
-    PathState ps{0u, 0u, 0u, f3s(0.0f), f3s(1.0f)};
-    Ray ray{};
-    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    uint32_t cur = 0, leaf_i = 0, leaf_end = 0;
-    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
-    // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
-    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
-    bool exhausted = false;                    // wave-uniform
-    uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
-    const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
-    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
-             u_rrounds = 0, u_rlanes = 0, u_other = 0, u_finw = 0, u_idlew = 0, u_parks = 0;
-
-    for (;;) {
-        uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        // ---- park ended traversals: exchange for a continuation, else take a free slot -----
-        {
-            const unsigned long long fin = __ballot(state == kFin);
-            if (fin) {
-                const uint32_t nf = (uint32_t)__popcll(fin);
-                const uint32_t x = min(nf, nt), y = min(nf - x, ne);
-                if (kStats) u_parks += x + y;
-                if (state == kFin) {
-                    const uint32_t rank = lane_rank(fin);
-                    if (rank < x) {
-                        const uint32_t slot = pv.tstack[nt - 1u - rank];
-                        Ray nr;
-                        PathState nps;
-                        pool_get_ray(pv, slot, nr, nps);
-                        pool_put_hit(pv, slot, ray, h, ps);
-                        pv.sstack[ns + rank] = slot;
-                        ray = nr;
-                        ps = nps;
-                        state = kTrav;
-                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                        cur = 0;
-                    } else if (rank < x + y) {
-                        const uint32_t slot = pv.fstack[ne - 1u - (rank - x)];
-                        pool_put_hit(pv, slot, ray, h, ps);
-                        pv.sstack[ns + rank] = slot;
-                        state = kIdle;
-                    }
-                }
-                nt -= x;
-                ne -= y;
-                ns += x + y;
-            }
-        }
-        // ---- idle lanes take waiting continuations --------------------------------------------
-        {
-            const unsigned long long idle = __ballot(state == kIdle);
-            if (idle != 0ull && nt > 0u) {
-                const uint32_t x = min((uint32_t)__popcll(idle), nt);
-                if (state == kIdle) {
-                    const uint32_t rank = lane_rank(idle);
-                    if (rank < x) {
-                        const uint32_t slot = pv.tstack[nt - 1u - rank];
-                        pool_get_ray(pv, slot, ray, ps);
-                        pv.fstack[ne + rank] = slot;
-                        state = kTrav;
-                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                        cur = 0;
-                    }
-                }
-                nt -= x;
-                ne += x;
-            }
-        }
-        // ---- new pixels (camera rays) for idle lanes -------------------------------------------
-        {
-            const uint32_t n_idle = popc_ballot(state == kIdle);
-            const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
-            if (!exhausted && n_idle > 0u && (n_idle >= kRefillMin || n_act == 0u)) {
-                if (kStats) {
-                    ++u_rrounds;
-                    u_rlanes += n_idle;
-                }
-                while (!exhausted) {
-                    const unsigned long long idle = __ballot(state == kIdle);
-                    if (idle == 0ull) break;
-                    if (chunk_used >= chunk_len) {
-                        if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                            exhausted = true;
-                            break;
-                        }
-                        chunk_used = 0;
-                    }
-                    const uint32_t rank = lane_rank(idle);
-                    const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
-                    if (state == kIdle && rank < take) {
-                        const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                        const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                        const uint32_t x = tx * 8u + (w & 7u),
-                                       row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
-                        const uint64_t g64 = (uint64_t)row * a.width + x;
-                        if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
-                            ps.gid = (uint32_t)g64;
-                            ps.seed = ps.gid + fh;  // kernel_bvh.cl:445
-                            ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, ps.seed);
-                            ps.radiance = f3s(0.0f);
-                            ps.beta = f3s(1.0f);
-                            ps.bounce = 0;
-                            if (bounces > 0u) {
-                                state = kTrav;
-                                h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                                cur = 0;
-                                if (kStats) ++st.rays;
-                            } else {
-                                finish_pixel<M>(a, ps.gid, f3s(0.0f), -1, 0.0f);  // no bounce: radiance 0
-                            }
-                        }
-                    }
-                    chunk_used += take;
-                }
-            }
-        }
-        uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats) cyc_refill += tB - tA;
-        // ---- shading: one record per lane, a full wave when the pool is full ------------------
-        // Only with no continuation waiting (nt == 0): then every lane owns a slot for the
-        // round -- its shade-ready record's, or a free one -- and parks its own in-flight state
-        // there while it shades, so the traversal registers are free for the shading code.
-        const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
-        if (nt == 0u && (ns >= kShadeMin || (ns > 0u && n_act < kLowWork))) {
-            const uint32_t nb = ns;  // <= 64; ne == 64 - nb
-            if (kStats) {
-                ++u_srounds;
-                u_slanes += nb;
-            }
-            const bool mine = lane < nb;
-            const uint32_t slot = mine ? pv.sstack[nb - 1u - lane] : pv.fstack[ne - 1u - (lane - nb)];
-            Ray sr;
-            Traversal sh;
-            PathState sp;
-            // Every lane runs the shading code (a lane without a record shades a miss and
-            // discards it): no divergent region around the large shading body, which keeps
-            // the register allocation of this loop close to the step schedule's.
-            pool_get_hit(pv, slot, sr, sh, sp);
-            if (!mine) sh.prim = -1;
-            pool_put_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
-            // compiler-only fences: keep the spill and the reload real (no store-to-load
-            // forwarding of the parked state across the shading code)
-            __asm__ volatile("" ::: "memory");
-            if (mine && sp.bounce == 0u && a.hitIds) {
-                a.hitIds[sp.gid] = sh.prim;
-                a.hitT[sp.gid] = sh.t;
-            }
-            LaneStats sst;
-            const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, sh, sr), sr, sp.radiance, sp.beta, sp.seed, sc,
-                                                      a, sst);
-            if (kStats && mine) st.hits += sst.hits;
-            ++sp.bounce;
-            const bool cont = mine && more && sp.bounce < bounces;
-            if (mine && !cont) {
-                finish_color<M>(a, sp.gid, F3{M::max(sp.radiance.x, 0.0f), M::max(sp.radiance.y, 0.0f),
-                                              M::max(sp.radiance.z, 0.0f)});
-            }
-            if (kStats && cont) ++st.rays;
-            __asm__ volatile("" ::: "memory");
-            pool_get_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
-            const unsigned long long cm = __ballot(cont);
-            const unsigned long long fm = __ballot(mine && !cont);
-            if (cont) {
-                pool_put_ray(pv, slot, sr, sp);
-                pv.tstack[lane_rank(cm)] = slot;
-            } else if (mine) {
-                pv.fstack[ne + lane_rank(fm)] = slot;
-            }
-            nt = (uint32_t)__popcll(cm);
-            ne += (uint32_t)__popcll(fm);
-            ns = 0;
-            if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tB;
-        }
-        if (n_act == 0u) {
-            if (exhausted && ns == 0u && nt == 0u && __ballot(state == kFin) == 0ull) break;
-            continue;
-        }
-
-        // ---- traversal steps (as in the step schedule) ----------------------------------------
-        for (;;) {
-            const uint32_t n_trav = popc_ballot(state == kTrav);
-            const uint32_t n_leaf = popc_ballot(state == kLeaf);
-            const uint32_t n_fin = popc_ballot(state == kFin);
-            if (n_trav + n_leaf == 0u) break;
-            if (n_fin >= kParkMin) break;
-            const uint32_t n_idle = 64u - n_trav - n_leaf - n_fin;
-            if (n_idle >= kRefillMin && (nt > 0u || !exhausted)) break;
-            if (nt == 0u && ns > 0u && n_trav + n_leaf < kLowWork) break;
-            const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
-            if (kStats) {
-                u_finw += n_fin;
-                u_idlew += n_idle;
-                u_other += leaf_step ? n_trav : n_leaf;
-                if (leaf_step) {
-                    ++u_tsteps;
-                    u_tlanes += n_leaf;
-                } else {
-                    ++u_nsteps;
-                    u_nlanes += n_trav;
-                }
-            }
-            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
-            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
-            if (!leaf_step) {
-#pragma unroll
-                for (int rep = 0; rep < kNodeBurst; ++rep) {
-                    if (state == kTrav) {
-                        if (kStats) ++st.visits;
-                        uint32_t next, first = 0, count = 0;
-                        if (kLdsScene) {
-                            uint32_t code;
-                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
-                                state = kLeaf;
-                                leaf_i = code;
-                            }
-                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
-                            state = kLeaf;
-                            leaf_i = first;
-                            leaf_end = first + count;
-                        }
-                        cur = next;
-                        if (state == kTrav && next == kEnd) state = kFin;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int rep = 0; rep < kTriBurst; ++rep) {
-                    if (state == kLeaf) {
-                        if (kStats) ++st.tests;
-                        if (kLdsScene) {
-                            const uint32_t idx = leaf_i & 0x00ffffffu;
-                            ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kFin : kTrav;
-                            leaf_i += 1u - (1u << 24);
-                        } else {
-                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                            ++leaf_i;
-                            if (leaf_i == leaf_end) state = cur == kEnd ? kFin : kTrav;
-                        }
-                    }
-                }
-            }
-        }
-        if (kStats) cyc_trav += __builtin_amdgcn_s_memtime() - tB;
-    }
-    if (kStats) {
-        flush_stats(a, st, (int)lane);
-        if (lane == 0) {
-            atomicAdd(&a.stats[4], (unsigned long long)cyc_refill);
-            atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
-            atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
-            atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
-            atomicAdd(&a.stats[8], (unsigned long long)u_nsteps);
-            atomicAdd(&a.stats[9], (unsigned long long)u_nlanes);
-            atomicAdd(&a.stats[10], (unsigned long long)u_tsteps);
-            atomicAdd(&a.stats[11], (unsigned long long)u_tlanes);
-            atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
-            atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
-            atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
-            atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
-            atomicAdd(&a.stats[16], (unsigned long long)u_other);
-            atomicAdd(&a.stats[17], (unsigned long long)u_finw);
-            atomicAdd(&a.stats[18], (unsigned long long)u_idlew);
-            atomicAdd(&a.stats[19], (unsigned long long)u_parks);
-        }
-    }
 }
 
 #ifdef RT_POOL_DEVICELIB_WAVES
@@ -1394,6 +44,7 @@ __global__ __launch_bounds__(256) RT_POOL_PINNED_OCC void kernel_entry_pool_pinn
     pool_body<MathPinned, kLdsScene, kStats>(a);
 }
 
+
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
 __global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1407,14 +58,7 @@ __global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __rest
 __global__ void pack_mats(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const rt_cl_material& m = in[i];
-    const float alpha = 2.0f / (m.roughness * m.roughness) - 2.0f;  // pow(r, 2.0f) == r * r
-    const float a2 = alpha * alpha;
-    // the shading step reads the first three 16-B words whole; the fourth is informational
-    out[4 * i] = make_float4(m.diffuse.x, m.diffuse.y, m.diffuse.z, 1.0f / (alpha + 1.0f));
-    out[4 * i + 1] = make_float4(m.specular.x, m.specular.y, m.specular.z, a2 * kInvPi);
-    out[4 * i + 2] = make_float4(m.emission.x, m.emission.y, m.emission.z, a2 - 1.0f);
-    out[4 * i + 3] = make_float4(m.roughness, alpha, 0.0f, 0.0f);
+    material_record<MathDeviceLib>(in[i], out + 4 * i);
 }
 
 __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
@@ -1435,7 +79,6 @@ __global__ void pack_tris(const rt_cl_triangle* __restrict__ in, float4* __restr
 namespace rtk {
 
 // Kernel variants: [schedule][math][scene in LDS][stats].
-using KernelFn = void (*)(KernelArgs);
 
 template <class M, bool L, bool S>
 static KernelFn pick_sched(int sched) {
@@ -1451,6 +94,7 @@ static KernelFn pick_sched(int sched) {
 }
 
 static KernelFn pick(int sched, int math, bool lds, bool stats) {
+    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats);
     if (math == MathDeviceLib::kId) {
         if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched) : pick_sched<MathDeviceLib, true, false>(sched);
         return stats ? pick_sched<MathDeviceLib, false, true>(sched) : pick_sched<MathDeviceLib, false, false>(sched);
@@ -1478,7 +122,13 @@ hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, 
     if (n_tris) hipLaunchKernelGGL(pack_tris, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, pt, n_tris);
     if (n_tris) hipLaunchKernelGGL(pack_shade, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, ps, n_tris);
     if (n_mats) hipLaunchKernelGGL(pack_mats, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);
+    // the shipped policy's material records (2.5-ulp divisions) follow the IEEE ones
+    if (n_mats) {
+        hipError_t e = launch_pack_mats_shipped(mats, n_mats, pm + 4 * (size_t)n_mats, st);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
 }  // namespace rtk
+

@@ -52,10 +52,16 @@ constexpr uint32_t kFinishWaveBytes = 64u * 16u;
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
 constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 
+using KernelFn = void (*)(KernelArgs);
+
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);
 int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
 hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
+
+// rt_kernels_shipped.hip: the MathShipped instantiations (own TU: OpenCL-default / and sqrt)
+KernelFn pick_shipped(int sched, bool lds, bool stats);
+hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk

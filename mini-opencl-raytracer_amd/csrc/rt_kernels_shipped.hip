@@ -1,0 +1,48 @@
+// rt_kernels_shipped.hip -- KernelEntry under the MathShipped policy: the reference kernel as
+// the AMD OpenCL compiler builds it by default (clBuildProgram(" -I . "), CLutils.cpp:52-66).
+//
+// The policy spells out every reference `/` and sqrt as the backend's OpenCL-accuracy
+// expansions (MathShipped::rcp/div/sqrt) and every fp-contract=on fusion as an fma at the
+// reference's expression site (madd, rt_math.hpp).  This TU is also compiled with
+// -fno-hip-fp32-correctly-rounded-divide-sqrt, so any division left to the compiler gets the
+// same OpenCL accuracy instead of the HIP default.  Only MathShipped is instantiated here.
+#include "rt_kernels_body.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtk {
+
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
+void kernel_entry_step_shipped(KernelArgs a) {
+    step_body<MathShipped, kLdsScene, kStats>(a);
+}
+template <bool kLdsScene, bool kStats>
+__global__ __launch_bounds__(256) void kernel_entry_pool_shipped(KernelArgs a) {
+    pool_body<MathShipped, kLdsScene, kStats>(a);
+}
+
+__global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    material_record<MathShipped>(in[i], out + 4 * i);
+}
+
+template <bool L, bool S>
+static KernelFn pick_sched_shipped(int sched) {
+    if (sched == kSchedStep) return kernel_entry_step_shipped<L, S>;
+    if (sched == kSchedPool) return kernel_entry_pool_shipped<L, S>;
+    return sched == kSchedRegen ? kernel_entry_regen<MathShipped, L, S> : kernel_entry<MathShipped, L, S>;
+}
+
+KernelFn pick_shipped(int sched, bool lds, bool stats) {
+    if (lds) return stats ? pick_sched_shipped<true, true>(sched) : pick_sched_shipped<true, false>(sched);
+    return stats ? pick_sched_shipped<false, true>(sched) : pick_sched_shipped<false, false>(sched);
+}
+
+hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
+    hipLaunchKernelGGL(pack_mats_shipped, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);
+    return hipGetLastError();
+}
+
+}  // namespace rtk

@@ -9,7 +9,15 @@
 //                pow/sin/cos/tan = __ocml_*_f32, max/min = llvm.maxnum/minnum.  This is
 //                the mode that is checked against the reference kernel itself, built by
 //                the image's OpenCL compiler and run through the OpenCL runtime
-//                (oracle/_ref, tests/test_ref_opencl.py).
+//                (oracle/_ref, tests/test_ref_opencl.py) with contraction off and
+//                correctly-rounded / and sqrt (the reference's `strict` build).
+// MathShipped  : devicelib builtins plus the two things the AMD OpenCL compiler does to the
+//                reference by default (clBuildProgram(" -I . "), CLutils.cpp:52-66): FP
+//                contraction within an expression (fp-contract=on: a*b + c -> fma at exactly
+//                the reference's source sites, `madd` below) and the 2.5-ulp `/` and 3-ulp
+//                sqrt of OpenCL C (no -cl-fp32-correctly-rounded-divide-sqrt).  The latter is
+//                a per-translation-unit setting, so this policy is instantiated only in
+//                rt_kernels_shipped.hip, compiled with -fno-hip-fp32-correctly-rounded-divide-sqrt.
 //
 // Everything here is compiled with -ffp-contract=off: each + - * / below is one IEEE
 // operation, in the association order the reference source spells out.
@@ -40,6 +48,11 @@ __device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
 // ---------------------------------------------------------------------------------------
 struct MathPinned {
     static constexpr int kId = 0;
+    static constexpr bool kContract = false;
+    // the reference's `/` and sqrt: IEEE, correctly rounded
+    __device__ __forceinline__ static float rcp(float x) { return 1.0f / x; }
+    __device__ __forceinline__ static float div(float a, float b) { return a / b; }
+    __device__ __forceinline__ static float sqrt(float x) { return __builtin_sqrtf(x); }
     __device__ __forceinline__ static float dot(F3 a, F3 b) {
         return (a.x * b.x + a.y * b.y) + a.z * b.z;
     }
@@ -61,6 +74,11 @@ struct MathPinned {
 
 struct MathDeviceLib {
     static constexpr int kId = 1;
+    static constexpr bool kContract = false;
+    // the reference's `/` and sqrt: IEEE, correctly rounded
+    __device__ __forceinline__ static float rcp(float x) { return 1.0f / x; }
+    __device__ __forceinline__ static float div(float a, float b) { return a / b; }
+    __device__ __forceinline__ static float sqrt(float x) { return __builtin_sqrtf(x); }
     // opencl.bc: dot = fma(z, z', fma(y, y', x*x'))
     __device__ __forceinline__ static float dot(F3 a, F3 b) {
         return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
@@ -84,6 +102,49 @@ struct MathDeviceLib {
     __device__ __forceinline__ static float max(float x, float y) { return __builtin_fmaxf(x, y); }
     __device__ __forceinline__ static float min(float x, float y) { return __builtin_fminf(x, y); }
 };
+
+struct MathShipped : MathDeviceLib {
+    static constexpr int kId = 2;
+    static constexpr bool kContract = true;
+    // OpenCL C's 2.5-ulp `/` and 3-ulp sqrt as the AMDGPU backend expands them with IEEE
+    // f32 denormals (AMDGPUCodeGenPrepare; read off the reference's shipped code object):
+    //   1/x  = ldexp(rcp(frexp_mant(x)), -frexp_exp(x))
+    //   a/b  = ldexp(frexp_mant(a) * rcp(frexp_mant(b)), frexp_exp(a) - frexp_exp(b))
+    //   sqrt = x < 2^-126 ? ldexp(v_sqrt(ldexp(x, 32)), -16) : v_sqrt(x)
+    // Spelled out with the hardware builtins rather than left to !fpmath metadata, which the
+    // optimizer drops when it hoists a loop-invariant division (the camera's 1/W, 1/H, W/H).
+    __device__ __forceinline__ static float rcp(float x) {
+        return __builtin_amdgcn_ldexpf(__builtin_amdgcn_rcpf(__builtin_amdgcn_frexp_mantf(x)),
+                                       -__builtin_amdgcn_frexp_expf(x));
+    }
+    __device__ __forceinline__ static float div(float a, float b) {
+        const float r = __builtin_amdgcn_rcpf(__builtin_amdgcn_frexp_mantf(b));
+        return __builtin_amdgcn_ldexpf(__builtin_amdgcn_frexp_mantf(a) * r,
+                                       __builtin_amdgcn_frexp_expf(a) - __builtin_amdgcn_frexp_expf(b));
+    }
+    __device__ __forceinline__ static float sqrt(float x) {
+        const bool scale = x < 0x1p-126f;
+        const float r = __builtin_amdgcn_sqrtf(__builtin_amdgcn_ldexpf(x, scale ? 32 : 0));
+        return __builtin_amdgcn_ldexpf(r, scale ? -16 : 0);
+    }
+};
+
+// A source-level `a * b + c` of the reference (one expression).  Under fp-contract=on clang
+// turns it into llvm.fmuladd (an fma on gfx950); where both operands of the + are products
+// the LEFT one is fused: `p*q + r*s` -> fma(p, q, r*s).  Callers spell each site in that form.
+template <class M>
+__device__ __forceinline__ float madd(float a, float b, float c) {
+    if (M::kContract) return __builtin_fmaf(a, b, c);
+    return a * b + c;
+}
+template <class M>
+__device__ __forceinline__ F3 madd(F3 a, F3 b, F3 c) {
+    return F3{madd<M>(a.x, b.x, c.x), madd<M>(a.y, b.y, c.y), madd<M>(a.z, b.z, c.z)};
+}
+template <class M>
+__device__ __forceinline__ F3 madd(F3 a, float b, F3 c) {
+    return F3{madd<M>(a.x, b, c.x), madd<M>(a.y, b, c.y), madd<M>(a.z, b, c.z)};
+}
 
 // normalize with the guard structure shared by both policies (see rt_pinned_math.h)
 template <class M>

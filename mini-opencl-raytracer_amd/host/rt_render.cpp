@@ -8,7 +8,7 @@
 // output is the bottom of the image, as glTexSubImage2D shows it).
 //
 // usage: rt_render [obj=path] [w=W] [h=H] [frames=N] [bounces=B] [light=T] [sky=S]
-//                  [out=file.ppm|file.png] [device=D] [math=pinned|devicelib]
+//                  [out=file.ppm|file.png] [device=D] [math=shipped|devicelib|pinned]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -47,13 +47,14 @@ int main(int argc, char** argv) {
     float skybox = (float)std::atof(arg(argc, argv, "sky", "1.0").c_str()); // CLRaytracer.h:34
     const std::string out = arg(argc, argv, "out", "render.ppm");
     const int device = std::atoi(arg(argc, argv, "device", "0").c_str());
-    const bool devlib = arg(argc, argv, "math", "pinned") == "devicelib";
+    const std::string math = arg(argc, argv, "math", "shipped");
+    const int math_mode = math == "pinned" ? RT_MATH_PINNED : math == "devicelib" ? RT_MATH_DEVICELIB : RT_MATH_SHIPPED;
 
     try {
         // CLRaytracer::Init (CLRaytracer.cpp:104-120)
         rtcl::CLContext ctx(device);
         auto kernel = std::make_shared<rtcl::CLKernel>(ctx, "KernelEntry");
-        if (devlib) rtcl::check(rtKernelSetMathMode(kernel->GetKernel(), RT_MATH_DEVICELIB), "math mode");
+        rtcl::check(rtKernelSetMathMode(kernel->GetKernel(), math_mode), "math mode");
         // CLRaytracer::SetupBuffers (CLRaytracer.cpp:122-137)
         int wi = (int)W, hi = (int)H;
         kernel->SetArgument(RenderKernelArgument_t::WIDTH, &wi, sizeof(int));

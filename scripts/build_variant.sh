@@ -9,8 +9,9 @@ OUT=$HERE/lib/variants; OBJ=$HERE/build/variants/$NAME
 mkdir -p $OUT $OBJ
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $FLAGS"
 /opt/rocm/bin/hipcc $F -c $HERE/csrc/rt_kernels.hip -o $OBJ/rt_kernels.o &
+/opt/rocm/bin/hipcc $F -fno-hip-fp32-correctly-rounded-divide-sqrt -c $HERE/csrc/rt_kernels_shipped.hip -o $OBJ/rt_kernels_shipped.o &
 /opt/rocm/bin/hipcc $F -c $HERE/csrc/rt_capi.cpp -o $OBJ/rt_capi.o &
 /opt/rocm/bin/hipcc $F -Wno-unused-result -c $HERE/csrc/rt_bvh.hip -o $OBJ/rt_bvh.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/librt_hip_$NAME.so $OBJ/rt_kernels.o $OBJ/rt_capi.o $OBJ/rt_bvh.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/librt_hip_$NAME.so $OBJ/rt_kernels.o $OBJ/rt_kernels_shipped.o $OBJ/rt_capi.o $OBJ/rt_bvh.o
 echo $OUT/librt_hip_$NAME.so

@@ -112,7 +112,7 @@ def test_frame_count_zero_path(cornell, oracle_mod):
     _assert_bits(rgb(got), rgb(want), "frame 0")
 
 
-@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB])
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB, N.MATH_SHIPPED])
 def test_schedules_agree_bit_exact(cornell, math):
     """Every schedule (tiles, path regeneration, step, LDS path pool) computes identical pixels,
     primary hits and counters."""
@@ -139,10 +139,11 @@ def test_zero_bounces_writes_black(cornell, oracle_mod):
     _assert_bits(rgb(got), rgb(want), "0 bounces")
 
 
-def test_global_scene_path_equals_lds_path(cornell):
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_SHIPPED])
+def test_global_scene_path_equals_lds_path(cornell, math):
     outs = []
     for force in (False, True):
-        r = HipRenderer(cornell, 256, 144, hits=True, force_global=force)
+        r = HipRenderer(cornell, 256, 144, math=math, hits=True, force_global=force)
         r.frame(1, light_bounces=9)
         r.frame(2, light_bounces=9)
         outs.append((r.result(), r.hits()[0], r.k.scene_in_lds()))

@@ -64,13 +64,16 @@ def test_proxy_pinned_bit_exact_vs_oracle(proxy, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_proxy_devicelib_equals_live_reference(proxy):
+@pytest.mark.parametrize("variant,math", [("strict", N.MATH_DEVICELIB), ("shipped", N.MATH_SHIPPED)])
+def test_proxy_equals_live_reference(proxy, variant, math):
+    """devicelib vs the strict reference build, shipped vs the default build: bit-exact on
+    the global-memory scene path (70k triangles)."""
     import clref
     ok, why = clref.available()
     if not ok:
         pytest.skip(why)
     try:
-        ref = clref.ReferenceKernel("strict")
+        ref = clref.ReferenceKernel(variant)
     except RuntimeError as e:
         pytest.skip(str(e))
     from hip_helpers import HipRenderer, rgb
@@ -78,12 +81,12 @@ def test_proxy_devicelib_equals_live_reference(proxy):
     want = ref.render(proxy, W, H, frames=(1, 2), light_bounces=9)[:, :3]
     ids_r, t_r = ref.primary_hits(proxy, W, H)
     ref.close()
-    r = HipRenderer(proxy, W, H, math=N.MATH_DEVICELIB)
+    r = HipRenderer(proxy, W, H, math=math)
     for f in (1, 2):
         r.frame(f, light_bounces=9)
     got = rgb(r.result())
     r.close()
-    h = HipRenderer(proxy, W, H, math=N.MATH_DEVICELIB, hits=True)
+    h = HipRenderer(proxy, W, H, math=math, hits=True)
     h.frame(1, light_bounces=1)
     ids, t = h.hits()
     h.close()
