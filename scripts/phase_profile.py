@@ -19,8 +19,11 @@ else:
 scheds = sys.argv[1:] or ["step"]
 for name in scheds:
   sched = {"step": N.SCHED_STEP, "pool": N.SCHED_POOL}[name]
-  for math in (N.MATH_DEVICELIB, N.MATH_PINNED):
-    for lb in (1, 9):
+  maths = [{"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[m]
+           for m in os.environ.get("RT_PHASE_MATH", "shipped,devicelib,pinned").split(",")]
+  lbs = [int(x) for x in os.environ.get("RT_PHASE_LB", "1,9").split(",")]
+  for math in maths:
+    for lb in lbs:
         r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=sched)
         r.frame(1, light_bounces=lb)
         r.ctx.Finish()
