@@ -38,6 +38,7 @@ from clrt import _native as N  # noqa: E402
 from clrt import multigpu as mg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
+SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMD-32
 CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
 
 
@@ -59,6 +60,10 @@ def parse():
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
     p.add_argument("--sched", choices=["regen", "tiles", "step", "pool"], default="step")
+    p.add_argument("--launch", choices=["fused", "per-frame"], default="fused",
+                   help="fused: the F frames of a step as one rtEnqueueKernelFrames call (one step launch "
+                        "over (frame, pixel) work items + the per-pixel accumulation); per-frame: one "
+                        "rtEnqueueKernel per frame, as the reference's RenderFrame loop. Same bits.")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-overlap", action="store_true",
@@ -109,7 +114,12 @@ class Rank:
         k.set_row_interleave(world, rank)
 
     def render(self):
-        """frames 1..F accumulated (RenderFrame's m_FrameCount sequence)."""
+        """frames 1..F accumulated (RenderFrame's m_FrameCount sequence): one launch per frame,
+        or (--launch fused, default) one rtEnqueueKernelFrames call -- the same bits."""
+        if self.args.launch == "fused":
+            self.k.set_uint(N.FRAME_COUNT, 1)
+            self.ctx.ExecuteKernelFrames(self.k, self.W * self.H, self.args.frames)
+            return
         for f in range(1, self.args.frames + 1):
             self.k.set_uint(N.FRAME_COUNT, f)
             self.ctx.ExecuteKernel(self.k, self.W * self.H)
@@ -294,18 +304,31 @@ def main():
     # rank's tile) / its mean duration
     launches = max(1, ks["launches"])
     kernel_ms = ks["kernel_ms"] / launches
+    accum_ms = ks["accum_ms"] / launches
+    frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
     local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
     tile_px = r.pixels
-    alg_bytes = (48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames + 32 * tile_px
+    alg_bytes = ((48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames
+                 + 32 * tile_px) * frames_per_launch
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     traffic = None
+    valu = None
     tpath = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            key = f"{args.scene}_{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
+            key = (f"{args.scene}_{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
+                   + ("_fused" if frames_per_launch > 1 else ""))
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
+                insts = tj[key].get("valu_insts_per_launch")
+                if insts and kernel_ms > 0:
+                    # VALU issue: one wave64 VALU instruction holds a SIMD-32 for 2 cycles; 4 SIMDs
+                    # per CU at the 2.4 GHz clock (MI355X_MICROARCH.md).  The binding resource of
+                    # this LDS-resident traversal, next to the HBM roofline the contract asks for.
+                    cap = SIMDS * 2.4e9 * kernel_ms * 1e-3 / 2.0
+                    valu = {"insts_per_launch": int(insts), "issue_frac": round(insts / cap, 4),
+                            "peak_insts_per_s": SIMDS * 2.4e9 / 2.0}
         except (ValueError, KeyError):
             traffic = None
 
@@ -342,7 +365,7 @@ def main():
                  "generated bunny-class proxy OBJ (clrt/proxy.py)") + "; rays generated in-kernel",
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "schedule": args.sched, "bvh": args.bvh, "parallelism": f"interleaved 8-row bands x{world}" + (
+                   "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh, "parallelism": f"interleaved 8-row bands x{world}" + (
                        (" + gloo gather to rank 0 (host-staged)" if args.dist_backend == "gloo" else
                         " + RCCL gather to rank 0" + ("" if args.no_overlap else ", pipelined with the next step"))
                        if dist is not None else ""),
@@ -350,7 +373,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
-                     "alg_bytes_per_launch": int(alg_bytes)},
+                     "frames_per_launch": frames_per_launch, "accum_ms_per_launch": round(accum_ms, 4),
+                     "alg_bytes_per_launch": int(alg_bytes), "valu": valu},
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(scene, args)

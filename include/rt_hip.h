@@ -88,6 +88,13 @@ int rtSetKernelArg(rt_kernel k, unsigned index, size_t size, const void* value);
  * pixel, 1-D NDRange of `global_work_size` (= width*height in the reference).
  * Asynchronous on the context's in-order stream. */
 int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size);
+/* Extension: frames FRAME_COUNT .. FRAME_COUNT + n_frames - 1 rendered and accumulated into
+ * BUFFER_OUT exactly as n_frames rtEnqueueKernel calls with those frame counts would (the
+ * reference's RenderFrame loop, CLRaytracer.cpp:35-47, without the per-frame read-back).  The
+ * step schedule runs them as ONE launch over (frame, pixel) work items -- one ramp-up and one
+ * drain instead of n_frames -- plus a per-pixel accumulation launch; other schedules launch
+ * per frame.  The FRAME_COUNT slot is left unchanged; hit buffers receive the last frame's. */
+int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames);
 
 /* CLContext::ReadBuffer (CLutils.cpp:37-42, non-blocking in the reference) and
  * CLContext::Finish (CLutils.h:122-125). */
@@ -175,6 +182,7 @@ typedef struct rt_stats {
      * then summed over all steps: lanes of the other traversal kind, lanes waiting to shade,
      * free lanes, reserved */
     uint64_t sched[12];
+    double accum_ms;   /* sum of the fused frames' accumulation launches (rtEnqueueKernelFrames) */
 } rt_stats;
 int rtKernelSetStats(rt_kernel k, int enable);
 int rtKernelSetTiming(rt_kernel k, int enable);

@@ -79,7 +79,7 @@ class Stats(ctypes.Structure):
                 ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("cycles_refill", ctypes.c_uint64), ("cycles_traverse", ctypes.c_uint64),
                 ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64),
-                ("sched", ctypes.c_uint64 * 12)]
+                ("sched", ctypes.c_uint64 * 12), ("accum_ms", ctypes.c_double)]
 
 
 _vp = ctypes.c_void_p
@@ -92,6 +92,7 @@ _HIP_PROTOS = {
     "rtReleaseKernel": (ctypes.c_int, [_vp]),
     "rtSetKernelArg": (ctypes.c_int, [_vp, ctypes.c_uint, ctypes.c_size_t, _vp]),
     "rtEnqueueKernel": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "rtEnqueueKernelFrames": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint]),
     "rtEnqueueReadBuffer": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, _vp]),
     "rtEnqueueWriteBuffer": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, _vp]),
     "rtFinish": (ctypes.c_int, [_vp]),

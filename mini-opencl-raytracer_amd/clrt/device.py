@@ -72,6 +72,12 @@ class CLContext:
         check(self._lib.rtEnqueueKernel(self.handle, kernel.handle, int(work_size)),
               "Failed to enqueue kernel")
 
+    def ExecuteKernelFrames(self, kernel: "CLKernel", work_size: int, n_frames: int) -> None:
+        """Extension: frames FRAME_COUNT .. FRAME_COUNT + n_frames - 1 (rtEnqueueKernelFrames),
+        bit-identical to n_frames ExecuteKernel calls with those frame counts."""
+        check(self._lib.rtEnqueueKernelFrames(self.handle, kernel.handle, int(work_size), int(n_frames)),
+              "Failed to enqueue kernel frames")
+
     def Finish(self) -> None:
         check(self._lib.rtFinish(self.handle), "Failed to finish queue")
 
@@ -189,7 +195,7 @@ class CLKernel:
         s = N.Stats()
         check(self._lib.rtKernelGetStats(self.handle, ctypes.byref(s)), "stats")
         return {"rays": s.rays, "node_visits": s.node_visits, "tri_tests": s.tri_tests,
-                "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms,
+                "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms, "accum_ms": s.accum_ms,
                 "cycles": {"refill": s.cycles_refill, "traverse": s.cycles_traverse,
                            "shade": s.cycles_shade, "total": s.cycles_total},
                 "sched": dict(zip(("node_steps", "node_lanes", "tri_steps", "tri_lanes", "shade_rounds",

@@ -78,14 +78,18 @@ struct rt_kernel_s {
                                                // (swept on MI355X: profiles/r01/chunk_sweep.txt)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
+    uint32_t* accum_key = nullptr;     // fused frames: sky-shortcut key state (4 words, zeroed once)
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
     unsigned long long* dstats = nullptr;  // device counters [4]
     uint64_t launches = 0;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;  // KernelEntry launches
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_accum;   // fused frames' accumulation
     std::vector<hipEvent_t> event_pool;
-    double kernel_ms = 0.0;
+    double kernel_ms = 0.0, accum_ms = 0.0;
+    float4* rad_buf = nullptr;  // fused frames: radiance per (frame slot, work-item)
+    size_t rad_buf_cap = 0;     // float4 slots
     // derived packed scene
     rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
@@ -390,18 +394,24 @@ hipEvent_t take_event(rt_kernel k) {
     return e;
 }
 
-int drain_events(rt_kernel k) {
-    for (auto& pr : k->pending_events) {
+static int drain_list(rt_kernel k, std::vector<std::pair<hipEvent_t, hipEvent_t>>& list, double& total) {
+    for (auto& pr : list) {
         float ms = 0.0f;
         hipError_t e = hipEventSynchronize(pr.second);
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
         if (e != hipSuccess) return map_hip(e);
-        k->kernel_ms += ms;
+        total += ms;
         k->event_pool.push_back(pr.first);
         k->event_pool.push_back(pr.second);
     }
-    k->pending_events.clear();
+    list.clear();
     return RT_SUCCESS;
+}
+
+int drain_events(rt_kernel k) {
+    int rc = drain_list(k, k->pending_events, k->kernel_ms);
+    if (rc) return rc;
+    return drain_list(k, k->pending_accum, k->accum_ms);
 }
 
 }  // namespace
@@ -521,6 +531,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     }
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
+    if (e == hipSuccess) e = hipMalloc(&k->accum_key, 16);
+    if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 16, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
@@ -536,10 +548,12 @@ int rtReleaseKernel(rt_kernel k) {
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
     (void)hipStreamSynchronize(k->ctx->stream);
-    for (auto& pr : k->pending_events) {
-        (void)hipEventDestroy(pr.first);
-        (void)hipEventDestroy(pr.second);
-    }
+    for (auto* list : {&k->pending_events, &k->pending_accum})
+        for (auto& pr : *list) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    if (k->rad_buf) (void)hipFree(k->rad_buf);
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
@@ -548,6 +562,7 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->shade_mats) (void)hipFree(k->shade_mats);
     if (k->dstats) (void)hipFree(k->dstats);
     if (k->work_counter) (void)hipFree(k->work_counter);
+    if (k->accum_key) (void)hipFree(k->accum_key);
     delete k;
     return RT_SUCCESS;
 }
@@ -572,7 +587,32 @@ int rtSetKernelArg(rt_kernel k, unsigned index, size_t size, const void* value) 
     return RT_SUCCESS;
 }
 
+static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_t n_frames);
+
 int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
+    return enqueue(ctx, k, global_work_size, 1);
+}
+
+int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames) {
+    if (n_frames == 0) return RT_INVALID_VALUE;
+    if (n_frames == 1 || !k || k->sched != RT_SCHED_STEP) {
+        // one launch per frame (the other schedules have no fused form): same results
+        if (!k) return RT_INVALID_KERNEL;
+        uint32_t f0;
+        std::memcpy(&f0, &k->u32[RT_ARG_FRAME_COUNT], 4);
+        int rc = RT_SUCCESS;
+        for (unsigned i = 0; i < n_frames && rc == RT_SUCCESS; ++i) {
+            const uint32_t f = f0 + i;
+            std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &f, 4);
+            rc = enqueue(ctx, k, global_work_size, 1);
+        }
+        std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &f0, 4);
+        return rc;
+    }
+    return enqueue(ctx, k, global_work_size, n_frames);
+}
+
+static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_t n_frames) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
     if (!k || k->ctx != ctx) return RT_INVALID_KERNEL;
@@ -646,6 +686,25 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     a.poolShadeMin = k->pool_shade;
     a.parkMin = k->park_min;
     a.lowWork = k->low_work;
+    a.nFrames = n_frames;
+    a.radStride = (uint32_t)g1;
+    a.radBuf = nullptr;
+    if (n_frames > 1) {
+        // fused frames: radiance slots indexed by global work-item id (the lane packs
+        // slot * g1 + gid into 32 bits); tiles x frames work items
+        if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xffffffffull)
+            return RT_INVALID_GLOBAL_WORK_SIZE;
+        const size_t need = (size_t)n_frames * g1;
+        if (k->rad_buf_cap < need) {
+            if (k->rad_buf) (void)hipFree(k->rad_buf);
+            k->rad_buf = nullptr;
+            k->rad_buf_cap = 0;
+            hipError_t me = hipMalloc(&k->rad_buf, need * sizeof(float4));
+            if (me != hipSuccess) return map_hip(me);
+            k->rad_buf_cap = need;
+        }
+        a.radBuf = k->rad_buf;
+    }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
@@ -656,7 +715,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
     const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
-                        (k->sched == RT_SCHED_STEP ? 4 * rtk::kFinishWaveBytes : 0);
+                        (k->sched == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math;
@@ -668,12 +727,12 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
-    grid = std::min<uint64_t>(grid, k->sched == RT_SCHED_TILES ? n_tiles : (n_tiles + 3) / 4);
+    grid = std::min<uint64_t>(grid, k->sched == RT_SCHED_TILES ? n_tiles : (n_tiles * n_frames + 3) / 4);
     if (grid == 0) grid = 1;
     {
         // bulk chunks only when every resident wave gets at least two of them; a small frame
         // (512x512: ~40 pixels per wave) is handed out 64 pixels at a time
-        const uint64_t tot = (uint64_t)a.nTiles * 64u, waves = grid * 4u;
+        const uint64_t tot = (uint64_t)a.nTiles * 64u * n_frames, waves = grid * 4u;
         a.chunkSplit = tot >= 2u * waves * k->chunk_pixels
                            ? (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels)
                            : 0u;
@@ -695,10 +754,26 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     if (k->timing) {
         (void)hipEventRecord(ev1, ctx->stream);
         k->pending_events.emplace_back(ev0, ev1);
-        if (k->pending_events.size() > 4096) {
-            rc = drain_events(k);
-            if (rc) return rc;
+    }
+    if (n_frames > 1) {
+        // fused frames: the gamma accumulation of every frame, in order, per pixel
+        hipEvent_t ea = nullptr, eb = nullptr;
+        if (k->timing) {
+            ea = take_event(k);
+            eb = take_event(k);
+            if (!ea || !eb) return RT_OUT_OF_RESOURCES;
+            (void)hipEventRecord(ea, ctx->stream);
         }
+        e = rtk::launch_accum_frames(a, k->math, k->accum_key, ctx->stream);
+        if (e != hipSuccess) return map_hip(e);
+        if (k->timing) {
+            (void)hipEventRecord(eb, ctx->stream);
+            k->pending_accum.emplace_back(ea, eb);
+        }
+    }
+    if (k->pending_events.size() + k->pending_accum.size() > 4096) {
+        rc = drain_events(k);
+        if (rc) return rc;
     }
     ++k->launches;
     return RT_SUCCESS;
@@ -867,6 +942,7 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     for (int i = 0; i < 12; ++i) out->sched[i] = h[8 + i];
     out->launches = k->launches;
     out->kernel_ms = k->kernel_ms;
+    out->accum_ms = k->accum_ms;
     return RT_SUCCESS;
 }
 
@@ -878,6 +954,7 @@ int rtKernelResetStats(rt_kernel k) {
     if (rc) return rc;
     k->launches = 0;
     k->kernel_ms = 0.0;
+    k->accum_ms = 0.0;
     hipError_t e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), k->ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
     return map_hip(e);

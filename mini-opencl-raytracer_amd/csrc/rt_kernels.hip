@@ -110,6 +110,28 @@ hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool ld
     return hipGetLastError();
 }
 
+template <class M>
+__global__ __launch_bounds__(256) void accum_frames(KernelArgs a, const uint32_t* key) {
+    accum_frames_body<M>(a, key);
+}
+template <class M>
+__global__ void accum_key(KernelArgs a, uint32_t* key) {
+    accum_key_body<M>(a, key);
+}
+
+hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st) {
+    if (math == MathShipped::kId) return launch_accum_frames_shipped(a, key, st);
+    const dim3 grid((a.nTiles + 4u * kAccumTilesPerWave - 1u) / (4u * kAccumTilesPerWave));
+    if (math == MathDeviceLib::kId) {
+        hipLaunchKernelGGL(accum_key<MathDeviceLib>, dim3(1), dim3(64), 0, st, a, key);
+        hipLaunchKernelGGL(accum_frames<MathDeviceLib>, grid, dim3(256), 0, st, a, key);
+    } else {
+        hipLaunchKernelGGL(accum_key<MathPinned>, dim3(1), dim3(64), 0, st, a, key);
+        hipLaunchKernelGGL(accum_frames<MathPinned>, grid, dim3(256), 0, st, a, key);
+    }
+    return hipGetLastError();
+}
+
 int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem) {
     int blocks = 0;
     KernelFn fn = pick(sched, math, lds, stats);

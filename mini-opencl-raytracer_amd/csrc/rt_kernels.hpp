@@ -40,6 +40,10 @@ struct KernelArgs {
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
     unsigned long long* stats;          // [rays, node visits, triangle tests, hits, 4 phase-cycle sums]
+    // rtEnqueueKernelFrames (step schedule): frames frameCount .. frameCount + nFrames - 1 in one
+    // launch; radiance per (frame slot, gid) in radBuf[slot * radStride + gid] (null: one frame)
+    float4* radBuf;
+    uint32_t nFrames, radStride;
 };
 
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
@@ -57,6 +61,10 @@ using KernelFn = void (*)(KernelArgs);
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);
 int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
+// accumulate the fused frames' radiances into the output (one pixel per lane)
+// (`key`: 4 words of per-kernel state for the sky shortcut, zeroed once; accum_key_body)
+hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st);
+hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipStream_t st);
 hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 

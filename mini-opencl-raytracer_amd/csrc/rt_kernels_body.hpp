@@ -457,20 +457,28 @@ __device__ __forceinline__ F3 render(const SceneView& sc, Ray ray,
     return F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
 }
 
-// kernel_bvh.cl:449-455: write (frameCount 0) or gamma-accumulate one work-item's result.
+// kernel_bvh.cl:449-455: the stored value for radiance `rad` over the stored value `old`
+// (frameCount 0: pow(rad, 0.45454545f), `old` unused; else the gamma accumulation).
+template <class M>
+__device__ __forceinline__ F3 gamma_out(uint32_t frameCount, F3 old, F3 rad) {
+    if (frameCount == 0)
+        return F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
+    const float fm1 = (float)(frameCount - 1), fc = (float)frameCount;
+    const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
+    const F3 num = madd<M>(lin, fm1, rad);
+    const F3 acc{M::div(num.x, fc), M::div(num.y, fc), M::div(num.z, fc)};
+    return F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+}
+
+// write (frameCount 0) or gamma-accumulate one work-item's result
 template <class M>
 __device__ __forceinline__ void finish_color(const KernelArgs& a, uint32_t gid, F3 rad) {
-    F3 out;
-    if (a.frameCount == 0) {
-        out = F3{M::pow(rad.x, 0.45454545f), M::pow(rad.y, 0.45454545f), M::pow(rad.z, 0.45454545f)};
-    } else {
-        const float4 old = a.result[gid];
-        const float fm1 = (float)(a.frameCount - 1), fc = (float)a.frameCount;
-        const F3 lin{M::pow(old.x, 2.2f), M::pow(old.y, 2.2f), M::pow(old.z, 2.2f)};
-        const F3 num = madd<M>(lin, fm1, rad);
-        const F3 acc{M::div(num.x, fc), M::div(num.y, fc), M::div(num.z, fc)};
-        out = F3{M::pow(acc.x, 0.454545f), M::pow(acc.y, 0.454545f), M::pow(acc.z, 0.454545f)};
+    F3 old = f3s(0.0f);
+    if (a.frameCount != 0) {
+        const float4 o = a.result[gid];
+        old = F3{o.x, o.y, o.z};
     }
+    const F3 out = gamma_out<M>(a.frameCount, old, rad);
     a.result[gid] = make_float4(out.x, out.y, out.z, 0.0f);
 }
 
@@ -723,9 +731,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
     const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
     const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
     const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;
+    // frames fused into this launch (rtEnqueueKernelFrames): work item = (frame slot, pixel);
+    // a finished path stores its radiance in radBuf[slot][gid] for accum_frames, and the lane's
+    // `gid` register then holds slot * radStride + gid
+    const bool fused = a.radBuf != nullptr;
+    const uint32_t total = a.nTiles * 64u * (fused ? a.nFrames : 1u);
     const uint32_t rowEnd = a.rowBegin + a.rowCount;
     const int lane = tid & 63;
     const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
@@ -765,7 +776,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 ++u_rrounds;
                 u_rlanes += n_free;
             }
-            // finished paths: hit outputs now, the gamma accumulation through the finish queue
+            // finished paths: the gamma accumulation through the finish queue, or (fused
+            // frames) the radiance into its frame slot
+            if (fused) {
+                if (state == kDone) {
+                    a.radBuf[gid] = make_float4(radiance.x, radiance.y, radiance.z, 0.0f);
+                    state = kIdle;
+                }
+            }
             const unsigned long long done = __ballot(state == kDone);
             if (done != 0ull) {
                 const uint32_t nd = (uint32_t)__popcll(done);
@@ -799,15 +817,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
                 if (state == kIdle && rank < take) {
                     const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                    const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
+                    uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
+                    const uint32_t slot = fused ? tile / a.nTiles : 0u;
+                    tile -= slot * a.nTiles;
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
                     const uint64_t g64 = (uint64_t)row * a.width + x;
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;
-                        seed = gid + fh;  // kernel_bvh.cl:445
+                        seed = gid + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
                         ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
+                        const bool last_frame = slot + 1u == a.nFrames;
+                        if (fused) gid += slot * a.radStride;
                         radiance = f3s(0.0f);
                         beta = f3s(1.0f);
                         bounce = 0;
@@ -818,9 +840,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             if (kStats) ++st.rays;
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
-                            if (a.hitIds) {
-                                a.hitIds[gid] = -1;
-                                a.hitT[gid] = 0.0f;
+                            if (a.hitIds && last_frame) {
+                                a.hitIds[(uint32_t)g64] = -1;
+                                a.hitT[(uint32_t)g64] = 0.0f;
                             }
                         }
                     }
@@ -918,9 +940,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
         }
         if (state == kShade) {
-            if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension)
-                a.hitIds[gid] = h.prim;
-                a.hitT[gid] = h.t;
+            if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension); fused: last frame's
+                const uint32_t last = (a.nFrames - 1u) * a.radStride;
+                if (!fused || gid >= last) {
+                    a.hitIds[gid - (fused ? last : 0u)] = h.prim;
+                    a.hitT[gid - (fused ? last : 0u)] = h.t;
+                }
             }
             const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, h, ray), ray, radiance, beta, seed, sc, a, st);
             ++bounce;
@@ -1363,6 +1388,106 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
             atomicAdd(&a.stats[18], (unsigned long long)u_idlew);
             atomicAdd(&a.stats[19], (unsigned long long)u_parks);
         }
+    }
+}
+
+// rtEnqueueKernelFrames: the gamma accumulation (kernel_bvh.cl:449-455) of frames
+// frameCount .. frameCount + nFrames - 1 in order, per pixel, from the radiances the fused step
+// launch left in radBuf[slot][gid].  Same pixel set as the step launch (8x8 tiles of the rank's
+// bands within the work range), same operations as nFrames per-frame launches.
+//
+// Sky pixels: a pixel whose every frame was a primary miss has radiance K_rad = max(1*0.5*sky
+// + 0, 0) in every component of every frame (kernel_bvh.cl:358-362, :383); if it also held
+// K_old, its result is one per-launch constant K_out = chain(K_old; K_rad x nFrames), computed
+// once by accum_key (one lane, same policy and operations).  Those pixels are written
+// directly; the others go through a per-wave LDS queue and are accumulated 64 at a time, so
+// the 6 pow per pixel and frame run on full waves of non-sky pixels only.  The key never
+// affects results, only how often the shortcut applies: K_old chains from the previous
+// launch's K_out (the value all-sky pixels then hold).
+// Key words: [0] valid, [1] K_rad bits, [2] K_old, [3] K_out.
+template <class M>
+__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, uint32_t gid) {
+    for (uint32_t s = 0; s < a.nFrames; ++s) {
+        const float4 r = a.radBuf[(size_t)s * a.radStride + gid];
+        v = gamma_out<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
+    }
+    return v;
+}
+
+template <class M>
+__device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* key) {
+    if (threadIdx.x != 0) return;
+    const float krad = M::max(madd<M>(1.0f, 0.5f * a.skyboxIntensity, 0.0f), 0.0f);
+    const float kold = key[0] == 1u ? __uint_as_float(key[3]) : 0.0f;
+    F3 v = f3s(kold);
+    for (uint32_t s = 0; s < a.nFrames; ++s) v = gamma_out<M>(a.frameCount + s, v, f3s(krad));
+    key[1] = __float_as_uint(krad);
+    key[2] = __float_as_uint(kold);
+    key[3] = __float_as_uint(v.x);  // three equal components: same inputs, same operations
+    key[0] = 1u;
+}
+
+constexpr uint32_t kAccumTilesPerWave = 8;   // 8x8 tiles per wave of the accumulation launch
+constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
+
+template <class M>
+__device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uint32_t* key) {
+    __shared__ uint32_t queue[4][kAccumQueue];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t* q = queue[wv];
+    uint32_t qn = 0;  // wave-uniform
+    const uint32_t krad = key[1], kold = key[2], kout = key[3];
+    const uint32_t tile0 = (blockIdx.x * 4u + wv) * kAccumTilesPerWave;
+    for (uint32_t t = 0; t < kAccumTilesPerWave; ++t) {
+        const uint32_t tile = tile0 + t;
+        if (tile >= a.nTiles) break;  // wave-uniform
+        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+        const uint32_t x = tx * 8u + (lane & 7u), row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (lane >> 3);
+        const uint64_t g64 = (uint64_t)row * a.width + x;
+        const bool live = x < a.width && row < a.rowBegin + a.rowCount && g64 >= a.gidBegin && g64 < a.gidEnd;
+        const uint32_t gid = (uint32_t)g64;
+        bool sky = false;
+        if (live) {
+            sky = true;
+            if (a.frameCount != 0u) {
+                const float4 o = a.result[gid];
+                sky = __float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold;
+            }
+            for (uint32_t s = 0; s < a.nFrames && sky; ++s) {
+                const float4 r = a.radBuf[(size_t)s * a.radStride + gid];
+                sky = __float_as_uint(r.x) == krad && __float_as_uint(r.y) == krad && __float_as_uint(r.z) == krad;
+            }
+            if (sky) {
+                const float v = __uint_as_float(kout);
+                a.result[gid] = make_float4(v, v, v, 0.0f);
+            }
+        }
+        const bool push = live && !sky;
+        const unsigned long long m = __ballot(push);
+        if (push) q[qn + lane_rank(m)] = gid;
+        qn += (uint32_t)__popcll(m);
+        if (qn >= 64u) {  // accumulate 64 queued pixels, one per lane
+            const uint32_t g = q[lane];
+            F3 v = f3s(0.0f);
+            if (a.frameCount != 0u) {
+                const float4 o = a.result[g];
+                v = F3{o.x, o.y, o.z};
+            }
+            v = accum_chain<M>(a, v, g);
+            a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
+            qn -= 64u;
+            if (lane < qn) q[lane] = q[64u + lane];
+        }
+    }
+    if (lane < qn) {
+        const uint32_t g = q[lane];
+        F3 v = f3s(0.0f);
+        if (a.frameCount != 0u) {
+            const float4 o = a.result[g];
+            v = F3{o.x, o.y, o.z};
+        }
+        v = accum_chain<M>(a, v, g);
+        a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
     }
 }
 

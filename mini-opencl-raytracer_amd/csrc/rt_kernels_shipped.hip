@@ -40,6 +40,20 @@ KernelFn pick_shipped(int sched, bool lds, bool stats) {
     return stats ? pick_sched_shipped<false, true>(sched) : pick_sched_shipped<false, false>(sched);
 }
 
+__global__ __launch_bounds__(256) void accum_frames_shipped(KernelArgs a, const uint32_t* key) {
+    accum_frames_body<MathShipped>(a, key);
+}
+__global__ void accum_key_shipped(KernelArgs a, uint32_t* key) {
+    accum_key_body<MathShipped>(a, key);
+}
+
+hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipStream_t st) {
+    const dim3 grid((a.nTiles + 4u * kAccumTilesPerWave - 1u) / (4u * kAccumTilesPerWave));
+    hipLaunchKernelGGL(accum_key_shipped, dim3(1), dim3(64), 0, st, a, key);
+    hipLaunchKernelGGL(accum_frames_shipped, grid, dim3(256), 0, st, a, key);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
     hipLaunchKernelGGL(pack_mats_shipped, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);
     return hipGetLastError();

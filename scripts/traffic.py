@@ -25,5 +25,9 @@ hbm = (2.0 * fetch + write) * 1024.0
 db = json.load(open(out)) if os.path.exists(out) else {}
 db[key] = {"hbm_bytes_per_launch": int(hbm), "fetch_size_kib": fetch, "write_size_kib": write, "kernel": k,
            "note": "(2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction"}
+for c, name in (("SQ_INSTS_VALU", "valu_insts_per_launch"), ("SQ_INSTS_LDS", "lds_insts_per_launch"),
+                ("SQ_INSTS_SALU", "salu_insts_per_launch"), ("GRBM_GUI_ACTIVE", "gui_active_cycles_all_xcds")):
+    if c in s[k]:
+        db[key][name] = int(s[k][c])
 json.dump(db, open(out, "w"), indent=1, sort_keys=True)
 print(key, db[key])

@@ -37,7 +37,9 @@ class HipRenderer:
             self.k.set_hit_buffers(*self.hit_bufs)
 
     def frame(self, frame_count, light_bounces=9, light_type=0, skybox=1.0, camera=DEFAULT_CAMERA,
-              work_range=None, interleave=None):
+              work_range=None, interleave=None, n_frames=None):
+        """One KernelEntry launch (RenderFrame), or with n_frames: frames frame_count ..
+        frame_count + n_frames - 1 through rtEnqueueKernelFrames."""
         k = self.k
         k.set_uint(N.FRAME_COUNT, frame_count)
         k.set_uint(N.FRAME_SEED, 12345)
@@ -51,7 +53,10 @@ class HipRenderer:
             k.set_work_range(*work_range)
         if interleave is not None:
             k.set_row_interleave(*interleave)
-        self.ctx.ExecuteKernel(k, self.n)
+        if n_frames is None:
+            self.ctx.ExecuteKernel(k, self.n)
+        else:
+            self.ctx.ExecuteKernelFrames(k, self.n, n_frames)
 
     def result(self):
         out = np.zeros((self.n, 4), np.float32)

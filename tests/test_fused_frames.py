@@ -1,0 +1,115 @@
+"""GPU: rtEnqueueKernelFrames -- F frames as one step launch over (frame, pixel) work items plus
+a per-pixel accumulation launch -- must leave exactly the bits of F per-frame launches
+(the reference's RenderFrame loop, CLRaytracer.cpp:35-47): output buffer, last frame's primary
+hits and the §8(d) counters, in every math mode, on the LDS and global scene paths, for band
+interleaves (multi-GPU ranks), work ranges and frame sequences starting at 0 or mid-way."""
+import numpy as np
+import pytest
+
+from clrt import _native as N
+from hip_helpers import HipRenderer, rgb
+
+pytestmark = pytest.mark.gpu
+
+
+def _render(scene, W, H, first, n, fused, math=N.MATH_SHIPPED, bounces=9, interleave=None,
+            work_range=None, force_global=False, sched=N.SCHED_STEP, pre=None):
+    r = HipRenderer(scene, W, H, math=math, hits=True, stats=True, force_global=force_global, sched=sched)
+    kw = dict(light_bounces=bounces, interleave=interleave, work_range=work_range)
+    if pre is not None:  # earlier frames already in the buffer
+        for f in pre:
+            r.frame(f, **kw)
+    r.k.reset_stats()
+    if fused:
+        r.frame(first, n_frames=n, **kw)
+    else:
+        for f in range(first, first + n):
+            r.frame(f, **kw)
+    out = (r.result(), r.hits(), r.k.stats())
+    r.close()
+    return out
+
+
+def _same(a, b):
+    assert a[0].tobytes() == b[0].tobytes(), f"{(a[0] != b[0]).any(axis=1).sum()} pixels differ"
+    assert np.array_equal(a[1][0], b[1][0]) and a[1][1].tobytes() == b[1][1].tobytes()
+    for key in ("rays", "node_visits", "tri_tests", "hits"):
+        assert a[2][key] == b[2][key], key
+
+
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB, N.MATH_SHIPPED])
+def test_fused_equals_per_frame(cornell, math):
+    W, H = 320, 180
+    _same(_render(cornell, W, H, 1, 8, True, math), _render(cornell, W, H, 1, 8, False, math))
+
+
+def test_fused_pinned_equals_oracle(cornell, oracle_mod):
+    W, H = 192, 108
+    got, (ids, t), _ = _render(cornell, W, H, 1, 4, True, N.MATH_PINNED, bounces=5)
+    res = np.zeros((W * H, 4), np.float32)
+    for f in range(1, 5):
+        res, wids, wt, _ = oracle_mod.render(cornell, W, H, frame_count=f, light_bounces=5, result=res,
+                                             want_hits=True, threads=16)
+    assert rgb(got).tobytes() == rgb(res).tobytes()
+    assert np.array_equal(ids, wids) and t.tobytes() == wt.tobytes()
+
+
+@pytest.mark.parametrize("first,n,pre", [(0, 3, None), (3, 5, (1, 2)), (1, 2, None)])
+def test_fused_frame_sequences(cornell, first, n, pre):
+    W, H = 200, 120
+    _same(_render(cornell, W, H, first, n, True, pre=pre), _render(cornell, W, H, first, n, False, pre=pre))
+
+
+@pytest.mark.parametrize("period,phase", [(2, 1), (8, 0), (8, 5)])
+def test_fused_band_interleave(cornell, period, phase):
+    W, H = 256, 200
+    _same(_render(cornell, W, H, 1, 6, True, interleave=(period, phase)),
+          _render(cornell, W, H, 1, 6, False, interleave=(period, phase)))
+
+
+def test_fused_work_range_and_global_path(cornell):
+    W, H = 240, 136
+    n = W * H
+    for wr, fg in (((n // 5, n - 77), False), ((0, n), True)):
+        _same(_render(cornell, W, H, 1, 5, True, work_range=wr, force_global=fg),
+              _render(cornell, W, H, 1, 5, False, work_range=wr, force_global=fg))
+
+
+def test_fused_bunny_proxy():
+    from clrt import proxy
+    sc = proxy.bunny_proxy()
+    W, H = 320, 180
+    _same(_render(sc, W, H, 1, 4, True), _render(sc, W, H, 1, 4, False))
+
+
+def test_fused_other_schedules_launch_per_frame(cornell):
+    W, H = 160, 96
+    _same(_render(cornell, W, H, 1, 3, True, sched=N.SCHED_REGEN), _render(cornell, W, H, 1, 3, False))
+
+
+def test_fused_sky_shortcut_chain(cornell):
+    """Repeated fused calls (the sky key chains from the previous call's result), a skybox change,
+    a math-mode switch and a restart at frame 1 over a non-sky history: every call's output equals
+    the per-frame launches (16:9 view: about half of the pixels see only sky)."""
+    W, H = 320, 180
+    seq = [(1, 4, 1.0, N.MATH_SHIPPED), (5, 4, 1.0, N.MATH_SHIPPED), (1, 8, 1.0, N.MATH_SHIPPED),
+           (1, 3, 0.6, N.MATH_SHIPPED), (4, 2, 0.6, N.MATH_DEVICELIB), (0, 2, 2.0, N.MATH_PINNED),
+           (1, 2, 2.0, N.MATH_PINNED)]
+    outs = []
+    for fused in (True, False):
+        r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, hits=True)
+        got = []
+        for first, n, sky, math in seq:
+            r.k.set_math_mode(math)
+            if fused:
+                r.frame(first, light_bounces=9, skybox=sky, n_frames=n)
+            else:
+                for f in range(first, first + n):
+                    r.frame(f, light_bounces=9, skybox=sky)
+            got.append(r.result())
+        ids, _ = r.hits()
+        r.close()
+        outs.append(got)
+    assert (ids < 0).mean() > 0.3
+    for a, b in zip(*outs):
+        assert a.tobytes() == b.tobytes()
