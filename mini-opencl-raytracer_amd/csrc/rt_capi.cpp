@@ -609,7 +609,19 @@ int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, 
         std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &f0, 4);
         return rc;
     }
-    return enqueue(ctx, k, global_work_size, n_frames);
+    // fused launches of at most kMaxFusedFrames frames each
+    uint32_t f0;
+    std::memcpy(&f0, &k->u32[RT_ARG_FRAME_COUNT], 4);
+    int rc = RT_SUCCESS;
+    for (unsigned done = 0; done < n_frames && rc == RT_SUCCESS;) {
+        const unsigned n = std::min<unsigned>(n_frames - done, rtk::kMaxFusedFrames);
+        const uint32_t f = f0 + done;
+        std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &f, 4);
+        rc = enqueue(ctx, k, global_work_size, n);
+        done += n;
+    }
+    std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &f0, 4);
+    return rc;
 }
 
 static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_t n_frames) {

@@ -51,6 +51,8 @@ constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
 constexpr int kSchedStep = 2;   // per-wave state machine: node / triangle steps, batched shading
 constexpr int kSchedPool = 3;   // step traversal + per-wave LDS path pool, full-wave shading
 constexpr int kNumSched = 4;
+// frames per fused launch (rtEnqueueKernelFrames splits longer runs)
+constexpr uint32_t kMaxFusedFrames = 8;
 // step schedule LDS per wave: the finish queue, 64 x {radiance, gid}
 constexpr uint32_t kFinishWaveBytes = 64u * 16u;
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks

@@ -1405,12 +1405,23 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
 // affects results, only how often the shortcut applies: K_old chains from the previous
 // launch's K_out (the value all-sky pixels then hold).
 // Key words: [0] valid, [1] K_rad bits, [2] K_old, [3] K_out.
+// the frame radiances of one pixel, all loads issued together (no dependent round trips)
+struct FrameRad {
+    float4 r[kMaxFusedFrames];
+};
+__device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gid) {
+    FrameRad f;
+#pragma unroll
+    for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
+        f.r[s] = s < a.nFrames ? a.radBuf[(size_t)s * a.radStride + gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return f;
+}
+
 template <class M>
-__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, uint32_t gid) {
-    for (uint32_t s = 0; s < a.nFrames; ++s) {
-        const float4 r = a.radBuf[(size_t)s * a.radStride + gid];
-        v = gamma_out<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
-    }
+__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, const FrameRad& f) {
+#pragma unroll
+    for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
+        if (s < a.nFrames) v = gamma_out<M>(a.frameCount + s, v, F3{f.r[s].x, f.r[s].y, f.r[s].z});
     return v;
 }
 
@@ -1448,15 +1459,14 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         const uint32_t gid = (uint32_t)g64;
         bool sky = false;
         if (live) {
-            sky = true;
-            if (a.frameCount != 0u) {
-                const float4 o = a.result[gid];
-                sky = __float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold;
-            }
-            for (uint32_t s = 0; s < a.nFrames && sky; ++s) {
-                const float4 r = a.radBuf[(size_t)s * a.radStride + gid];
-                sky = __float_as_uint(r.x) == krad && __float_as_uint(r.y) == krad && __float_as_uint(r.z) == krad;
-            }
+            const float4 o = a.frameCount != 0u ? a.result[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const FrameRad f = load_frames(a, gid);
+            sky = a.frameCount == 0u ||
+                  (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold);
+#pragma unroll
+            for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
+                sky = sky && (s >= a.nFrames || (__float_as_uint(f.r[s].x) == krad && __float_as_uint(f.r[s].y) == krad &&
+                                                 __float_as_uint(f.r[s].z) == krad));
             if (sky) {
                 const float v = __uint_as_float(kout);
                 a.result[gid] = make_float4(v, v, v, 0.0f);
@@ -1468,12 +1478,8 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         qn += (uint32_t)__popcll(m);
         if (qn >= 64u) {  // accumulate 64 queued pixels, one per lane
             const uint32_t g = q[lane];
-            F3 v = f3s(0.0f);
-            if (a.frameCount != 0u) {
-                const float4 o = a.result[g];
-                v = F3{o.x, o.y, o.z};
-            }
-            v = accum_chain<M>(a, v, g);
+            const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g));
             a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
             qn -= 64u;
             if (lane < qn) q[lane] = q[64u + lane];
@@ -1481,12 +1487,8 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
     }
     if (lane < qn) {
         const uint32_t g = q[lane];
-        F3 v = f3s(0.0f);
-        if (a.frameCount != 0u) {
-            const float4 o = a.result[g];
-            v = F3{o.x, o.y, o.z};
-        }
-        v = accum_chain<M>(a, v, g);
+        const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g));
         a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
     }
 }

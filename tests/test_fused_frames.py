@@ -54,7 +54,7 @@ def test_fused_pinned_equals_oracle(cornell, oracle_mod):
     assert np.array_equal(ids, wids) and t.tobytes() == wt.tobytes()
 
 
-@pytest.mark.parametrize("first,n,pre", [(0, 3, None), (3, 5, (1, 2)), (1, 2, None)])
+@pytest.mark.parametrize("first,n,pre", [(0, 3, None), (3, 5, (1, 2)), (1, 2, None), (1, 11, None)])
 def test_fused_frame_sequences(cornell, first, n, pre):
     W, H = 200, 120
     _same(_render(cornell, W, H, first, n, True, pre=pre), _render(cornell, W, H, first, n, False, pre=pre))
