@@ -261,11 +261,9 @@ def main():
         counts = tot.cpu().numpy()
 
     def step():
-        r.render()
+        r.render()  # N = 1: steps are queued back to back (sync only around the timed region)
         if gather is not None:
             gather()
-        else:
-            r.finish()
 
     def steps(n):
         for _ in range(n):
