@@ -708,6 +708,11 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_NODE_BURST
 #define RT_NODE_BURST 6
 #endif
+// diagnostic (stats variant, scripts/timeline.py): wave start/end timeline instead of the
+// lane-wait counters
+#ifndef RT_TIMELINE
+#define RT_TIMELINE 0
+#endif
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
 #endif
@@ -763,6 +768,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
+#if RT_TIMELINE
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
     // diagnostic lane-utilisation counters (wave-uniform): steps / rounds and lanes served
     uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
              u_rrounds = 0, u_rlanes = 0, u_other = 0, u_shadew = 0, u_freew = 0, u_pad = 0;
@@ -976,11 +984,28 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
             atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
             atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
+#if RT_TIMELINE
+            // diagnostic timeline (100 MHz device clock; scripts/timeline.py): last wave start,
+            // first wave start (complemented), last wave end, sum of wave ends, waves, and a
+            // wave lifetime histogram (20 us bins) after the hit-id words (the caller sizes that
+            // buffer W*H + 64)
+            const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
+            atomicMax(&a.stats[15], (unsigned long long)rt_start);
+            atomicMax(&a.stats[16], (unsigned long long)~rt_start);
+            atomicMax(&a.stats[17], (unsigned long long)rt_end);
+            atomicAdd(&a.stats[18], (unsigned long long)rt_end);
+            atomicAdd(&a.stats[19], 1ull);
+            if (a.hitIds) {
+                const uint32_t bin = min((uint32_t)((rt_end - rt_start) / 2000ull), 63u);
+                atomicAdd(&a.hitIds[a.width * a.height + bin], 1);
+            }
+#else
             atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
             atomicAdd(&a.stats[16], (unsigned long long)u_other);
             atomicAdd(&a.stats[17], (unsigned long long)u_shadew);
             atomicAdd(&a.stats[18], (unsigned long long)u_freew);
             atomicAdd(&a.stats[19], (unsigned long long)u_pad);
+#endif
         }
     }
 }

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Diagnostic (needs a build with -DRT_TIMELINE=1, scripts/build_variant.sh, via RT_HIP_LIB):
+launch span vs mean wave end of the instrumented step launch -- how much of a launch is the
+drain (waves finished, GPU waiting for the last ones).  usage: timeline.py [N ...]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mini-opencl-raytracer_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import clrt  # noqa: E402
+from clrt import _native as N  # noqa: E402
+from hip_helpers import HipRenderer  # noqa: E402
+
+sc = clrt.scene.cornell()
+for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
+    for fused in (False, True):
+        r = HipRenderer(sc, 3840, 2160, math=N.MATH_SHIPPED, stats=True)
+        r.k.set_row_interleave(n, 0)
+        npx = 3840 * 2160
+        hb = (r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 64) * 4), r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 64) * 4))
+        r.k.set_hit_buffers(*hb)
+        r.k.reset_stats()
+        if fused:
+            r.frame(1, light_bounces=9, n_frames=8)
+        else:
+            r.frame(1, light_bounces=9)
+        r.ctx.Finish()
+        s = r.k.stats()["sched"]
+        t0 = (~s["other_lanes"]) & 0xffffffffffffffff
+        t1, tsum, waves = s["shade_wait"], s["free_wait"], s["reserved"]
+        last_start = (s["refill_lanes"] - t0) / 100.0
+        span = (t1 - t0) / 100.0
+        mean_end = (tsum / max(1, waves) - t0) / 100.0
+        print(f"N={n} {'fused x8' if fused else 'one frame'}: waves {waves}, span {span:.1f} us, "
+              f"last wave start {last_start:.1f} us, mean wave end {mean_end:.1f} us, drain {span - mean_end:.1f} us ({(span - mean_end) / span:.1%})",
+              flush=True)
+        import numpy as np
+        h = np.zeros(npx + 64, np.int32)
+        r.ctx.ReadBuffer(hb[0], h, blocking=True)
+        hist = h[npx:]
+        print("   wave lifetime histogram (20 us bins, from the first nonempty): " +
+              " ".join(str(int(x)) for x in hist[np.nonzero(hist)[0][0]:np.nonzero(hist)[0][-1] + 1]), flush=True)
+        r.k.set_hit_buffers(None, None)
+        for x in hb:
+            x.release()
+        r.close()
