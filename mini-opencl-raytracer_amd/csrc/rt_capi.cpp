@@ -90,6 +90,7 @@ struct rt_kernel_s {
     double kernel_ms = 0.0, accum_ms = 0.0;
     float4* rad_buf = nullptr;  // fused frames: radiance per (frame slot, work-item)
     size_t rad_buf_cap = 0;     // float4 slots
+    uint8_t* frame_flags = nullptr;  // fused frames: primary-miss flag per (frame slot, work-item)
     // derived packed scene
     rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
@@ -554,6 +555,7 @@ int rtReleaseKernel(rt_kernel k) {
             (void)hipEventDestroy(pr.second);
         }
     if (k->rad_buf) (void)hipFree(k->rad_buf);
+    if (k->frame_flags) (void)hipFree(k->frame_flags);
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
@@ -709,13 +711,17 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         const size_t need = (size_t)n_frames * g1;
         if (k->rad_buf_cap < need) {
             if (k->rad_buf) (void)hipFree(k->rad_buf);
+            if (k->frame_flags) (void)hipFree(k->frame_flags);
             k->rad_buf = nullptr;
+            k->frame_flags = nullptr;
             k->rad_buf_cap = 0;
             hipError_t me = hipMalloc(&k->rad_buf, need * sizeof(float4));
+            if (me == hipSuccess) me = hipMalloc(&k->frame_flags, need);
             if (me != hipSuccess) return map_hip(me);
             k->rad_buf_cap = need;
         }
         a.radBuf = k->rad_buf;
+        a.frameFlags = k->frame_flags;
     }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;

@@ -43,6 +43,7 @@ struct KernelArgs {
     // rtEnqueueKernelFrames (step schedule): frames frameCount .. frameCount + nFrames - 1 in one
     // launch; radiance per (frame slot, gid) in radBuf[slot * radStride + gid] (null: one frame)
     float4* radBuf;
+    uint8_t* frameFlags;                // [slot * radStride + gid]: 1 = radiance (K_rad x3), not in radBuf
     uint32_t nFrames, radStride;
 };
 

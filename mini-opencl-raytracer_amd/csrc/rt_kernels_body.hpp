@@ -742,6 +742,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // `gid` register then holds slot * radStride + gid
     const bool fused = a.radBuf != nullptr;
     const uint32_t total = a.nTiles * 64u * (fused ? a.nFrames : 1u);
+    // the radiance of a primary miss, max(1 * 0.5*skybox + 0, 0) per component (kernel_bvh.cl:360, :383)
+    const float krad = M::max(madd<M>(1.0f, 0.5f * a.skyboxIntensity, 0.0f), 0.0f);
     const uint32_t rowEnd = a.rowBegin + a.rowCount;
     const int lane = tid & 63;
     const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
@@ -788,7 +790,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             // frames) the radiance into its frame slot
             if (fused) {
                 if (state == kDone) {
-                    a.radBuf[gid] = make_float4(radiance.x, radiance.y, radiance.z, 0.0f);
+                    // a radiance of (K_rad, K_rad, K_rad) -- a primary miss -- is only flagged
+                    const bool skyv = __float_as_uint(radiance.x) == __float_as_uint(krad) &&
+                                      __float_as_uint(radiance.y) == __float_as_uint(krad) &&
+                                      __float_as_uint(radiance.z) == __float_as_uint(krad);
+                    if (!skyv) a.radBuf[gid] = make_float4(radiance.x, radiance.y, radiance.z, 0.0f);
+                    a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
             }
@@ -1430,15 +1437,24 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
 // affects results, only how often the shortcut applies: K_old chains from the previous
 // launch's K_out (the value all-sky pixels then hold).
 // Key words: [0] valid, [1] K_rad bits, [2] K_old, [3] K_out.
-// the frame radiances of one pixel, all loads issued together (no dependent round trips)
+// the frame radiances of one pixel, all loads issued together (no dependent round trips); a
+// flagged frame (frameFlags: radiance (K_rad, K_rad, K_rad), not stored) reads as K_rad
 struct FrameRad {
     float4 r[kMaxFusedFrames];
 };
-__device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gid) {
+__device__ __forceinline__ uint32_t load_flags(const KernelArgs& a, uint32_t gid) {
+    uint32_t fl = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
+        if (s < a.nFrames) fl |= (uint32_t)a.frameFlags[(size_t)s * a.radStride + gid] << s;
+    return fl;
+}
+__device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gid, uint32_t flags, float krad) {
     FrameRad f;
 #pragma unroll
     for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
-        f.r[s] = s < a.nFrames ? a.radBuf[(size_t)s * a.radStride + gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        f.r[s] = (s < a.nFrames && !((flags >> s) & 1u)) ? a.radBuf[(size_t)s * a.radStride + gid]
+                                                          : make_float4(krad, krad, krad, 0.0f);
     return f;
 }
 
@@ -1472,7 +1488,8 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t* q = queue[wv];
     uint32_t qn = 0;  // wave-uniform
-    const uint32_t krad = key[1], kold = key[2], kout = key[3];
+    const uint32_t kold = key[2], kout = key[3];
+    const float krf = __uint_as_float(key[1]);
     const uint32_t tile0 = (blockIdx.x * 4u + wv) * kAccumTilesPerWave;
     for (uint32_t t = 0; t < kAccumTilesPerWave; ++t) {
         const uint32_t tile = tile0 + t;
@@ -1485,13 +1502,10 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         bool sky = false;
         if (live) {
             const float4 o = a.frameCount != 0u ? a.result[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const FrameRad f = load_frames(a, gid);
-            sky = a.frameCount == 0u ||
-                  (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold);
-#pragma unroll
-            for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
-                sky = sky && (s >= a.nFrames || (__float_as_uint(f.r[s].x) == krad && __float_as_uint(f.r[s].y) == krad &&
-                                                 __float_as_uint(f.r[s].z) == krad));
+            const uint32_t fl = load_flags(a, gid);
+            sky = fl == (1u << a.nFrames) - 1u &&
+                  (a.frameCount == 0u ||
+                   (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold));
             if (sky) {
                 const float v = __uint_as_float(kout);
                 a.result[gid] = make_float4(v, v, v, 0.0f);
@@ -1504,7 +1518,7 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         if (qn >= 64u) {  // accumulate 64 queued pixels, one per lane
             const uint32_t g = q[lane];
             const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g));
+            const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
             a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
             qn -= 64u;
             if (lane < qn) q[lane] = q[64u + lane];
@@ -1513,7 +1527,7 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
     if (lane < qn) {
         const uint32_t g = q[lane];
         const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g));
+        const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
         a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
     }
 }
