@@ -111,7 +111,7 @@ hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool ld
 }
 
 template <class M>
-__global__ __launch_bounds__(256) void accum_frames(KernelArgs a, const uint32_t* key) {
+__global__ __launch_bounds__(256) RT_ACCUM_OCC void accum_frames(KernelArgs a, const uint32_t* key) {
     accum_frames_body<M>(a, key);
 }
 template <class M>

@@ -1479,6 +1479,12 @@ __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* ke
     key[0] = 1u;
 }
 
+// accumulation launch occupancy (A/B builds: -DRT_ACCUM_WAVES=n)
+#ifdef RT_ACCUM_WAVES
+#define RT_ACCUM_OCC __attribute__((amdgpu_waves_per_eu(RT_ACCUM_WAVES, 8)))
+#else
+#define RT_ACCUM_OCC
+#endif
 constexpr uint32_t kAccumTilesPerWave = 8;   // 8x8 tiles per wave of the accumulation launch
 constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
 

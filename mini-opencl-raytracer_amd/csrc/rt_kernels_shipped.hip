@@ -40,7 +40,7 @@ KernelFn pick_shipped(int sched, bool lds, bool stats) {
     return stats ? pick_sched_shipped<false, true>(sched) : pick_sched_shipped<false, false>(sched);
 }
 
-__global__ __launch_bounds__(256) void accum_frames_shipped(KernelArgs a, const uint32_t* key) {
+__global__ __launch_bounds__(256) RT_ACCUM_OCC void accum_frames_shipped(KernelArgs a, const uint32_t* key) {
     accum_frames_body<MathShipped>(a, key);
 }
 __global__ void accum_key_shipped(KernelArgs a, uint32_t* key) {
