@@ -7,7 +7,7 @@ NAME=$1; FLAGS=${2:-}
 HERE=$(cd "$(dirname "$0")/../mini-opencl-raytracer_amd" && pwd)
 OUT=$HERE/lib/variants; OBJ=$HERE/build/variants/$NAME
 mkdir -p $OUT $OBJ
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize $FLAGS"
+F="--offload-arch=gfx950 -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize $FLAGS"
 /opt/rocm/bin/hipcc $F -c $HERE/csrc/rt_kernels.hip -o $OBJ/rt_kernels.o &
 /opt/rocm/bin/hipcc $F -fno-hip-fp32-correctly-rounded-divide-sqrt -c $HERE/csrc/rt_kernels_shipped.hip -o $OBJ/rt_kernels_shipped.o &
 /opt/rocm/bin/hipcc $F -c $HERE/csrc/rt_capi.cpp -o $OBJ/rt_capi.o &
