@@ -102,7 +102,7 @@ struct rt_kernel_s {
     bool oct_ok = false;               // every leaf fits the records' inline {first, count}
     float4* g_nodes = nullptr;         // global-scene node records (64 B, top of the tree first)
     size_t g_nodes_cap = 0;
-    uint32_t n_top = 0, top_limit = 256;  // nodes of g_nodes staged in LDS (global path)
+    uint32_t n_top = 0, top_limit = 384;  // nodes of g_nodes staged in LDS (global path; swept, profiles/r01/bunny_top_nodes_sweep_2.txt)
     size_t packed_tris_cap = 0, oct_nodes_cap = 0;
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
