@@ -10,10 +10,16 @@ namespace rtk {
 // Entry points per math policy: the devicelib body fits 80 VGPRs with a small spill, and
 // 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
 // (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
-template <bool kLdsScene, bool kStats>
+// (LDS scenes 5 waves per SIMD, scenes read from HBM/L2 6, as for the shipped policy)
+template <bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
-void kernel_entry_step_devicelib(KernelArgs a) {
-    step_body<MathDeviceLib, kLdsScene, kStats>(a);
+void kernel_entry_step_devicelib_lds(KernelArgs a) {
+    step_body<MathDeviceLib, true, kStats>(a);
+}
+template <bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
+void kernel_entry_step_devicelib_global(KernelArgs a) {
+    step_body<MathDeviceLib, false, kStats>(a);
 }
 #ifdef RT_STEP_PINNED_WAVES
 #define RT_STEP_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
@@ -83,7 +89,7 @@ namespace rtk {
 template <class M, bool L, bool S>
 static KernelFn pick_sched(int sched) {
     if (sched == kSchedStep) {
-        if (M::kId == MathDeviceLib::kId) return kernel_entry_step_devicelib<L, S>;
+        if (M::kId == MathDeviceLib::kId) return L ? kernel_entry_step_devicelib_lds<S> : kernel_entry_step_devicelib_global<S>;
         return kernel_entry_step_pinned<L, S>;
     }
     if (sched == kSchedPool) {

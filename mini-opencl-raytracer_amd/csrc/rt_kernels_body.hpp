@@ -42,6 +42,9 @@
 #ifndef RT_STEP_DEVICELIB_WAVES
 #define RT_STEP_DEVICELIB_WAVES 5
 #endif
+#ifndef RT_STEP_GLOBAL_WAVES
+#define RT_STEP_GLOBAL_WAVES 6  // the same entry points for scenes read from HBM/L2
+#endif
 
 namespace rtk {
 

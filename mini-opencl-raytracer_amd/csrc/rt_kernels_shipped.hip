@@ -12,10 +12,17 @@
 
 namespace rtk {
 
-template <bool kLdsScene, bool kStats>
+// LDS-resident scenes run 5 waves per SIMD (VALU-bound); scenes read from HBM/L2 run 6 (load
+// latency to hide: bunny proxy -2.4 %, profiles/r01/global_path_waves_ab.txt)
+template <bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
-void kernel_entry_step_shipped(KernelArgs a) {
-    step_body<MathShipped, kLdsScene, kStats>(a);
+void kernel_entry_step_shipped_lds(KernelArgs a) {
+    step_body<MathShipped, true, kStats>(a);
+}
+template <bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
+void kernel_entry_step_shipped_global(KernelArgs a) {
+    step_body<MathShipped, false, kStats>(a);
 }
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) void kernel_entry_pool_shipped(KernelArgs a) {
@@ -30,7 +37,7 @@ __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4*
 
 template <bool L, bool S>
 static KernelFn pick_sched_shipped(int sched) {
-    if (sched == kSchedStep) return kernel_entry_step_shipped<L, S>;
+    if (sched == kSchedStep) return L ? kernel_entry_step_shipped_lds<S> : kernel_entry_step_shipped_global<S>;
     if (sched == kSchedPool) return kernel_entry_pool_shipped<L, S>;
     return sched == kSchedRegen ? kernel_entry_regen<MathShipped, L, S> : kernel_entry<MathShipped, L, S>;
 }
