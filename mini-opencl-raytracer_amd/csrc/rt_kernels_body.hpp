@@ -1461,11 +1461,17 @@ __device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gi
     return f;
 }
 
+// The frame loop is NOT unrolled: one gamma step is ~6 ocml pow of ~120 instructions each, and
+// the unrolled 8-frame chain (twice, with the tail flush) made a 17k-instruction kernel whose
+// waves missed the instruction cache.  The frames stay loaded up front and rotate through r[0].
 template <class M>
-__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, const FrameRad& f) {
+__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, FrameRad f) {
+#pragma unroll 1
+    for (uint32_t s = 0; s < a.nFrames; ++s) {
+        v = gamma_out<M>(a.frameCount + s, v, F3{f.r[0].x, f.r[0].y, f.r[0].z});
 #pragma unroll
-    for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
-        if (s < a.nFrames) v = gamma_out<M>(a.frameCount + s, v, F3{f.r[s].x, f.r[s].y, f.r[s].z});
+        for (uint32_t k = 0; k + 1 < kMaxFusedFrames; ++k) f.r[k] = f.r[k + 1];
+    }
     return v;
 }
 
@@ -1488,7 +1494,10 @@ __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* ke
 #else
 #define RT_ACCUM_OCC
 #endif
-constexpr uint32_t kAccumTilesPerWave = 8;   // 8x8 tiles per wave of the accumulation launch
+#ifndef RT_ACCUM_TPW
+#define RT_ACCUM_TPW 1
+#endif
+constexpr uint32_t kAccumTilesPerWave = RT_ACCUM_TPW;  // 8x8 tiles per wave of the accumulation launch
 constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
 
 template <class M>
@@ -1524,20 +1533,19 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         const unsigned long long m = __ballot(push);
         if (push) q[qn + lane_rank(m)] = gid;
         qn += (uint32_t)__popcll(m);
-        if (qn >= 64u) {  // accumulate 64 queued pixels, one per lane
-            const uint32_t g = q[lane];
-            const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
-            a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
-            qn -= 64u;
+        const bool last = t + 1 == kAccumTilesPerWave || tile + 1 >= a.nTiles;
+        // accumulate up to 64 queued pixels, one per lane; after the wave's last tile, until empty
+        // (one call site: the chain is the bulk of the kernel's code)
+        while (qn >= 64u || (last && qn > 0u)) {
+            if (lane < qn) {
+                const uint32_t g = q[lane];
+                const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
+                a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
+            }
+            qn = qn >= 64u ? qn - 64u : 0u;
             if (lane < qn) q[lane] = q[64u + lane];
         }
-    }
-    if (lane < qn) {
-        const uint32_t g = q[lane];
-        const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
-        a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
     }
 }
 
