@@ -304,6 +304,10 @@ def main():
     kernel_ms = ks["kernel_ms"] / launches
     accum_ms = ks["accum_ms"] / launches
     frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
+    # fused launches accumulate on a second stream that overlaps the next render (rt_capi.cpp,
+    # RT_ACCUM_OVERLAP): its event span then includes the wait for the render, so it is not a
+    # kernel duration -- the rocprofv3 kernel trace under profiles/ carries that
+    accum_overlapped = frames_per_launch > 1 and os.environ.get("RT_ACCUM_OVERLAP", "1") != "0"
     local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
     tile_px = r.pixels
     alg_bytes = ((48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames
@@ -371,7 +375,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
-                     "frames_per_launch": frames_per_launch, "accum_ms_per_launch": round(accum_ms, 4),
+                     "frames_per_launch": frames_per_launch, "accum_ms_per_launch": None if accum_overlapped else round(accum_ms, 4),
+                     "accum_overlapped": accum_overlapped,
                      "alg_bytes_per_launch": int(alg_bytes), "valu": valu},
     }
     if world == 1 and not args.no_cpu_baseline:

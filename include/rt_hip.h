@@ -93,7 +93,11 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size);
  * reference's RenderFrame loop, CLRaytracer.cpp:35-47, without the per-frame read-back).  The
  * step schedule runs them as ONE launch over (frame, pixel) work items -- one ramp-up and one
  * drain instead of n_frames -- plus a per-pixel accumulation launch; other schedules launch
- * per frame.  The FRAME_COUNT slot is left unchanged; hit buffers receive the last frame's. */
+ * per frame.  The FRAME_COUNT slot is left unchanged; hit buffers receive the last frame's.
+ * The accumulation launch runs on a second stream of the context, overlapping the next
+ * fused render; every other call on the context (buffer reads/writes/copies, per-frame
+ * launches, rtFinish, rtContextGetStream) is ordered after it, so the context still behaves
+ * as one in-order queue.  RT_ACCUM_OVERLAP=0 in the environment keeps it on the main stream. */
 int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames);
 
 /* CLContext::ReadBuffer (CLutils.cpp:37-42, non-blocking in the reference) and
@@ -182,7 +186,8 @@ typedef struct rt_stats {
      * then summed over all steps: lanes of the other traversal kind, lanes waiting to shade,
      * free lanes, reserved */
     uint64_t sched[12];
-    double accum_ms;   /* sum of the fused frames' accumulation launches (rtEnqueueKernelFrames) */
+    double accum_ms;   /* sum of the fused frames' accumulation launches (rtEnqueueKernelFrames);
+                        * when overlapped (default) the spans include the wait for the render */
 } rt_stats;
 int rtKernelSetStats(rt_kernel k, int enable);
 int rtKernelSetTiming(rt_kernel k, int enable);
@@ -198,7 +203,9 @@ int rtKernelForceGlobalScene(rt_kernel k, int force);
  * collective's staging tensor), asynchronous on the context's stream. */
 int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem src, size_t offset, size_t size, void* dst_device);
 
-/* Device address of a buffer and the context's HIP stream (for collectives/interop). */
+/* Device address of a buffer and the context's HIP stream (for collectives/interop).  The
+ * stream is returned after pending fused-frame accumulations have been ordered into it; work
+ * enqueued on it directly after a later rtEnqueueKernelFrames must call this again first. */
 int rtBufferGetDevicePointer(rt_mem mem, void** dptr);
 int rtBufferGetSize(rt_mem mem, size_t* size);
 int rtContextGetStream(rt_context ctx, void** hip_stream);

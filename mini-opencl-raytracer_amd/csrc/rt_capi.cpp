@@ -50,7 +50,26 @@ struct rt_context_s {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 0;
+    // Fused frames: the accumulation launch runs on its own stream, so it overlaps the next
+    // render (its waves fit beside the render grid: RT_ACCUM_VGPRS).  Every other operation
+    // goes through qs(), which first makes the context's in-order stream wait for the
+    // accumulations enqueued so far -- to the caller the context stays one in-order queue.
+    hipStream_t astream = nullptr;
+    hipEvent_t atail = nullptr;  // last accumulation enqueued on astream
+    bool apending = false;
+    bool overlap = true;  // RT_ACCUM_OVERLAP=0: accumulate on the main stream
 };
+
+namespace {
+// The context's stream, after every pending accumulation (see rt_context_s).
+hipStream_t qs(rt_context ctx) {
+    if (ctx->apending) {
+        (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
+        ctx->apending = false;
+    }
+    return ctx->stream;
+}
+}  // namespace
 
 struct rt_mem_s {
     rt_context ctx = nullptr;
@@ -88,9 +107,15 @@ struct rt_kernel_s {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_accum;   // fused frames' accumulation
     std::vector<hipEvent_t> event_pool;
     double kernel_ms = 0.0, accum_ms = 0.0;
-    float4* rad_buf = nullptr;  // fused frames: radiance per (frame slot, work-item)
-    size_t rad_buf_cap = 0;     // float4 slots
-    uint8_t* frame_flags = nullptr;  // fused frames: primary-miss flag per (frame slot, work-item)
+    // fused frames: radiance and primary-miss flag per (frame slot, work-item), two sets used
+    // alternately so a render can run while the previous launch's accumulation reads the other
+    float4* rad_buf[2] = {};
+    uint8_t* frame_flags[2] = {};
+    size_t rad_buf_cap[2] = {};        // float4 slots
+    hipEvent_t rad_free[2] = {};       // recorded on astream after the accumulation reading the set
+    bool rad_busy[2] = {};
+    int rad_set = 0;
+    hipEvent_t render_done = nullptr;  // recorded on the main stream after a fused render
     // derived packed scene
     rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
@@ -125,8 +150,8 @@ int host_bytes(rt_mem m, std::vector<uint8_t>& tmp, const uint8_t** out) {
         return RT_SUCCESS;
     }
     tmp.resize(m->size);
-    hipError_t e = hipMemcpyAsync(tmp.data(), m->dptr, m->size, hipMemcpyDeviceToHost, m->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(m->ctx->stream);
+    hipError_t e = hipMemcpyAsync(tmp.data(), m->dptr, m->size, hipMemcpyDeviceToHost, qs(m->ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(m->ctx));
     if (e != hipSuccess) return map_hip(e);
     *out = tmp.data();
     return RT_SUCCESS;
@@ -339,7 +364,7 @@ int prepare_scene(rt_kernel k) {
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->g_nodes, gn.data(), gn.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                      k->ctx->stream);
+                                      qs(k->ctx));
         if (e != hipSuccess) return map_hip(e);
     }
     std::vector<uint32_t> oct;
@@ -348,8 +373,8 @@ int prepare_scene(rt_kernel k) {
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
-                                      hipMemcpyHostToDevice, k->ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+                                      hipMemcpyHostToDevice, qs(k->ctx));
+        if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
         if (e != hipSuccess) return map_hip(e);
     }
     if (k->packed_tris_cap < (size_t)nt) {
@@ -367,7 +392,7 @@ int prepare_scene(rt_kernel k) {
     if (rc) return rc;
     hipError_t e = rtk::launch_pack(static_cast<const rt_cl_triangle*>(tm->dptr), nt, k->packed_tris,
                                     k->shade_tris, static_cast<const rt_cl_material*>(mm->dptr), nmat,
-                                    k->shade_mats, k->ctx->stream);
+                                    k->shade_mats, qs(k->ctx));
     if (e != hipSuccess) return map_hip(e);
     k->n_nodes = nn;
     k->n_tris = nt;
@@ -431,10 +456,15 @@ int rtCreateContext(int device_index, rt_context* out) {
     if (!c) return RT_OUT_OF_HOST_MEMORY;
     c->device = device_index;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->astream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->atail, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->astream) (void)hipStreamDestroy(c->astream);
         delete c;
         return RT_INVALID_COMMAND_QUEUE;
     }
+    if (const char* v = std::getenv("RT_ACCUM_OVERLAP")) c->overlap = std::atoi(v) != 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device_index) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     if (c->num_cus <= 0) c->num_cus = 256;
@@ -445,8 +475,11 @@ int rtCreateContext(int device_index, rt_context* out) {
 int rtReleaseContext(rt_context ctx) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
-    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(qs(ctx));
+    (void)hipStreamSynchronize(ctx->astream);
     (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->astream);
+    (void)hipEventDestroy(ctx->atail);
     delete ctx;
     return RT_SUCCESS;
 }
@@ -480,11 +513,11 @@ int rtCreateBuffer(rt_context ctx, uint64_t flags, size_t size, const void* host
             return RT_OUT_OF_HOST_MEMORY;
         }
         m->shadow_valid = true;
-        e = hipMemcpyAsync(m->dptr, host_ptr, size, hipMemcpyHostToDevice, ctx->stream);
+        e = hipMemcpyAsync(m->dptr, host_ptr, size, hipMemcpyHostToDevice, qs(ctx));
     } else {
-        e = hipMemsetAsync(m->dptr, 0, size, ctx->stream);
+        e = hipMemsetAsync(m->dptr, 0, size, qs(ctx));
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(ctx));
     if (e != hipSuccess) {
         (void)hipFree(m->dptr);
         delete m;
@@ -498,7 +531,7 @@ int rtReleaseBuffer(rt_mem m) {
     if (!m) return RT_INVALID_MEM_OBJECT;
     int rc = ensure_device(m->ctx);
     if (rc) return rc;
-    (void)hipStreamSynchronize(m->ctx->stream);
+    (void)hipStreamSynchronize(qs(m->ctx));
     (void)hipFree(m->dptr);
     delete m;
     return RT_SUCCESS;
@@ -533,9 +566,9 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 16);
-    if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 16, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 16, qs(ctx));
+    if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(ctx));
     if (e != hipSuccess) {
         delete k;
         return map_hip(e);
@@ -548,14 +581,19 @@ int rtReleaseKernel(rt_kernel k) {
     if (!k) return RT_INVALID_KERNEL;
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
-    (void)hipStreamSynchronize(k->ctx->stream);
+    (void)hipStreamSynchronize(qs(k->ctx));
     for (auto* list : {&k->pending_events, &k->pending_accum})
         for (auto& pr : *list) {
             (void)hipEventDestroy(pr.first);
             (void)hipEventDestroy(pr.second);
         }
-    if (k->rad_buf) (void)hipFree(k->rad_buf);
-    if (k->frame_flags) (void)hipFree(k->frame_flags);
+    (void)hipStreamSynchronize(k->ctx->astream);
+    for (int i = 0; i < 2; ++i) {
+        if (k->rad_buf[i]) (void)hipFree(k->rad_buf[i]);
+        if (k->frame_flags[i]) (void)hipFree(k->frame_flags[i]);
+        if (k->rad_free[i]) (void)hipEventDestroy(k->rad_free[i]);
+    }
+    if (k->render_done) (void)hipEventDestroy(k->render_done);
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
@@ -643,6 +681,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         return RT_INVALID_MEM_OBJECT;
     rc = prepare_scene(k);
     if (rc) return rc;
+    // a per-frame launch read-modify-writes the output: after the pending accumulations
+    if (n_frames == 1) (void)qs(ctx);
 
     uint64_t g0 = std::min<uint64_t>(k->range_first, global_work_size);
     uint64_t g1 = k->range_last ? std::min<uint64_t>(k->range_last, global_work_size) : global_work_size;
@@ -709,19 +749,33 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xffffffffull)
             return RT_INVALID_GLOBAL_WORK_SIZE;
         const size_t need = (size_t)n_frames * g1;
-        if (k->rad_buf_cap < need) {
-            if (k->rad_buf) (void)hipFree(k->rad_buf);
-            if (k->frame_flags) (void)hipFree(k->frame_flags);
-            k->rad_buf = nullptr;
-            k->frame_flags = nullptr;
-            k->rad_buf_cap = 0;
-            hipError_t me = hipMalloc(&k->rad_buf, need * sizeof(float4));
-            if (me == hipSuccess) me = hipMalloc(&k->frame_flags, need);
+        const int rs = ctx->overlap ? k->rad_set : 0;
+        if (k->rad_buf_cap[rs] < need) {
+            // the set may still be read by an accumulation in flight
+            hipError_t me = hipStreamSynchronize(ctx->astream);
             if (me != hipSuccess) return map_hip(me);
-            k->rad_buf_cap = need;
+            if (k->rad_buf[rs]) (void)hipFree(k->rad_buf[rs]);
+            if (k->frame_flags[rs]) (void)hipFree(k->frame_flags[rs]);
+            k->rad_buf[rs] = nullptr;
+            k->frame_flags[rs] = nullptr;
+            k->rad_buf_cap[rs] = 0;
+            me = hipMalloc(&k->rad_buf[rs], need * sizeof(float4));
+            if (me == hipSuccess) me = hipMalloc(&k->frame_flags[rs], need);
+            if (me == hipSuccess && !k->rad_free[rs])
+                me = hipEventCreateWithFlags(&k->rad_free[rs], hipEventDisableTiming);
+            if (me == hipSuccess && !k->render_done)
+                me = hipEventCreateWithFlags(&k->render_done, hipEventDisableTiming);
+            if (me != hipSuccess) return map_hip(me);
+            k->rad_buf_cap[rs] = need;
         }
-        a.radBuf = k->rad_buf;
-        a.frameFlags = k->frame_flags;
+        // the render writes the set: after the accumulation that last read it
+        if (k->rad_busy[rs]) {
+            hipError_t me = hipStreamWaitEvent(ctx->stream, k->rad_free[rs], 0);
+            if (me != hipSuccess) return map_hip(me);
+            k->rad_busy[rs] = false;
+        }
+        a.radBuf = k->rad_buf[rs];
+        a.frameFlags = k->frame_flags[rs];
     }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
@@ -774,19 +828,37 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         k->pending_events.emplace_back(ev0, ev1);
     }
     if (n_frames > 1) {
-        // fused frames: the gamma accumulation of every frame, in order, per pixel
+        // fused frames: the gamma accumulation of every frame, in order, per pixel -- on the
+        // accumulation stream after this render, overlapping whatever the main stream runs next
+        // (the next fused render uses the other radiance set); qs() joins it back
+        hipStream_t as = ctx->stream;
+        if (ctx->overlap) {
+            as = ctx->astream;
+            e = hipEventRecord(k->render_done, ctx->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(as, k->render_done, 0);
+            if (e != hipSuccess) return map_hip(e);
+        }
         hipEvent_t ea = nullptr, eb = nullptr;
         if (k->timing) {
             ea = take_event(k);
             eb = take_event(k);
             if (!ea || !eb) return RT_OUT_OF_RESOURCES;
-            (void)hipEventRecord(ea, ctx->stream);
+            (void)hipEventRecord(ea, as);
         }
-        e = rtk::launch_accum_frames(a, k->math, k->accum_key, ctx->stream);
+        e = rtk::launch_accum_frames(a, k->math, k->accum_key, as);
         if (e != hipSuccess) return map_hip(e);
         if (k->timing) {
-            (void)hipEventRecord(eb, ctx->stream);
+            (void)hipEventRecord(eb, as);
             k->pending_accum.emplace_back(ea, eb);
+        }
+        if (ctx->overlap) {
+            const int rs = k->rad_set;
+            e = hipEventRecord(k->rad_free[rs], as);
+            if (e == hipSuccess) e = hipEventRecord(ctx->atail, as);
+            if (e != hipSuccess) return map_hip(e);
+            k->rad_busy[rs] = true;
+            k->rad_set ^= 1;
+            ctx->apending = true;
         }
     }
     if (k->pending_events.size() + k->pending_accum.size() > 4096) {
@@ -811,8 +883,8 @@ int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in
     if (e != hipSuccess) return map_hip(e);
     uint32_t count = 0;
     e = rtb::build(static_cast<rt_cl_triangle*>(tris->dptr), (uint32_t)n_tris, mp,
-                   static_cast<rt_cl_bvh_node*>(nodes->dptr), &count, scratch, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+                   static_cast<rt_cl_bvh_node*>(nodes->dptr), &count, scratch, qs(ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(ctx));
     (void)hipFree(scratch);
     if (e != hipSuccess) return map_hip(e);
     for (rt_mem m : {tris, nodes}) {  // device contents changed: host shadows are stale
@@ -829,8 +901,8 @@ int rtEnqueueReadBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, s
     if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
     if (!dst || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
     hipError_t e = hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
-                                  hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && blocking) e = hipStreamSynchronize(ctx->stream);
+                                  hipMemcpyDeviceToHost, qs(ctx));
+    if (e == hipSuccess && blocking) e = hipStreamSynchronize(qs(ctx));
     return map_hip(e);
 }
 
@@ -843,8 +915,8 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, 
     if (m->shadow_valid) std::memcpy(m->shadow.data() + offset, src, size);
     ++m->generation;
     hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(m->dptr) + offset, src, size,
-                                  hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess && blocking) e = hipStreamSynchronize(ctx->stream);
+                                  hipMemcpyHostToDevice, qs(ctx));
+    if (e == hipSuccess && blocking) e = hipStreamSynchronize(qs(ctx));
     return map_hip(e);
 }
 
@@ -854,13 +926,13 @@ int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem m, size_t offset, size_t
     if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
     if (!dst || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
     return map_hip(hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
-                                  hipMemcpyDeviceToDevice, ctx->stream));
+                                  hipMemcpyDeviceToDevice, qs(ctx)));
 }
 
 int rtFinish(rt_context ctx) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
-    return map_hip(hipStreamSynchronize(ctx->stream));
+    return map_hip(hipStreamSynchronize(qs(ctx)));
 }
 
 int rtKernelSetMathMode(rt_kernel k, int mode) {
@@ -895,7 +967,7 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
     if (src_offset + (rows - 1) * src_pitch + width_bytes > src->size) return RT_INVALID_VALUE;
     return map_hip(hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
-                                    width_bytes, rows, hipMemcpyDeviceToDevice, ctx->stream));
+                                    width_bytes, rows, hipMemcpyDeviceToDevice, qs(ctx)));
 }
 
 int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src_pitch, rt_mem dst,
@@ -907,7 +979,7 @@ int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
     if (dst_offset + (rows - 1) * dst_pitch + width_bytes > dst->size) return RT_INVALID_VALUE;
     return map_hip(hipMemcpy2DAsync(static_cast<uint8_t*>(dst->dptr) + dst_offset, dst_pitch, src, src_pitch,
-                                    width_bytes, rows, hipMemcpyDeviceToDevice, ctx->stream));
+                                    width_bytes, rows, hipMemcpyDeviceToDevice, qs(ctx)));
 }
 
 int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {
@@ -944,8 +1016,8 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
     unsigned long long h[kStatWords] = {};
-    hipError_t e = hipMemcpyAsync(h, k->dstats, sizeof(h), hipMemcpyDeviceToHost, k->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+    hipError_t e = hipMemcpyAsync(h, k->dstats, sizeof(h), hipMemcpyDeviceToHost, qs(k->ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
     if (e != hipSuccess) return map_hip(e);
     rc = drain_events(k);
     if (rc) return rc;
@@ -973,8 +1045,8 @@ int rtKernelResetStats(rt_kernel k) {
     k->launches = 0;
     k->kernel_ms = 0.0;
     k->accum_ms = 0.0;
-    hipError_t e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), k->ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(k->ctx->stream);
+    hipError_t e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(k->ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
     return map_hip(e);
 }
 
@@ -1004,7 +1076,7 @@ int rtBufferGetSize(rt_mem m, size_t* size) {
 
 int rtContextGetStream(rt_context ctx, void** s) {
     if (!ctx || !s) return RT_INVALID_VALUE;
-    *s = ctx->stream;
+    *s = qs(ctx);
     return RT_SUCCESS;
 }
 

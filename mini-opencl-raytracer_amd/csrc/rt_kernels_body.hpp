@@ -1475,6 +1475,20 @@ __device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, FrameRad f)
     return v;
 }
 
+// The same chain with each frame's radiance loaded when its step runs: few registers, so the
+// accumulation waves fit beside a running render grid (RT_ACCUM_VGPRS, co-resident overlap;
+// rt_capi.cpp).  Same values, same operations, same order.
+template <class M>
+__device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32_t gid, uint32_t flags, float krad) {
+#pragma unroll 1
+    for (uint32_t s = 0; s < a.nFrames; ++s) {
+        const float4 r = ((flags >> s) & 1u) ? make_float4(krad, krad, krad, 0.0f)
+                                             : a.radBuf[(size_t)s * a.radStride + gid];
+        v = gamma_out<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
+    }
+    return v;
+}
+
 template <class M>
 __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* key) {
     if (threadIdx.x != 0) return;
@@ -1488,9 +1502,16 @@ __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* ke
     key[0] = 1u;
 }
 
-// accumulation launch occupancy (A/B builds: -DRT_ACCUM_WAVES=n)
+// accumulation launch occupancy (A/B builds: -DRT_ACCUM_WAVES=n, -DRT_ACCUM_VGPRS=n)
+#ifndef RT_ACCUM_VGPRS
+#define RT_ACCUM_VGPRS 32
+#endif
 #ifdef RT_ACCUM_WAVES
 #define RT_ACCUM_OCC __attribute__((amdgpu_waves_per_eu(RT_ACCUM_WAVES, 8)))
+#elif RT_ACCUM_VGPRS
+// a register cap that fits one accumulation wave per SIMD beside the render grid (5 waves of
+// 96 VGPRs on the LDS path, 6 of 80 on the global path: 32 of 512 left)
+#define RT_ACCUM_OCC __attribute__((amdgpu_num_vgpr(RT_ACCUM_VGPRS)))
 #else
 #define RT_ACCUM_OCC
 #endif
@@ -1540,7 +1561,11 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
             if (lane < qn) {
                 const uint32_t g = q[lane];
                 const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#if RT_ACCUM_VGPRS
+                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, g, load_flags(a, g), krf);
+#else
                 const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
+#endif
                 a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
             }
             qn = qn >= 64u ? qn - 64u : 0u;

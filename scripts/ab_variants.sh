@@ -8,7 +8,7 @@ m=$1; shift
 one() {  # one <label> [env...]
   local label=$1; shift
   out=$(env "$@" timeout -k 10 120 python bench.py --math $m --no-cpu-baseline --steps 3 --warmup 1 "${EXTRA[@]}") || exit $?
-  echo "$m $label $(echo $out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_frame"], d["roofline"].get("accum_ms_per_launch"))')"
+  echo "$m $label $(echo $out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_frame"], d["roofline"]["kernel_ms"])')"
 }
 EXTRA=("$@")
 for rep in 1 2; do

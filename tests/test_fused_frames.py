@@ -113,3 +113,35 @@ def test_fused_sky_shortcut_chain(cornell):
     assert (ids < 0).mean() > 0.3
     for a, b in zip(*outs):
         assert a.tobytes() == b.tobytes()
+
+
+def test_overlapped_accumulation_stays_in_order(cornell):
+    """The accumulation of a fused launch runs on a second stream beside the next render
+    (rt_capi.cpp qs()); mixing fused launches, per-frame launches, many back-to-back fused
+    launches (both radiance sets in flight) and a host write of the output between them must
+    still give the bits of one in-order queue of per-frame launches."""
+    W, H = 224, 128
+    a = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    b = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    for r, fused in ((a, True), (b, False)):
+        def run(first, n):
+            if fused:
+                r.frame(first, n_frames=n, light_bounces=9)
+            else:
+                for f in range(first, first + n):
+                    r.frame(f, light_bounces=9)
+        run(1, 8)
+        run(9, 1)
+        run(10, 3)
+        run(13, 4)
+        run(17, 2)
+        mid = r.result()  # read between launches: joins the pending accumulation
+        run(19, 5)
+        r.ctx.WriteBuffer(r.out, mid)  # host overwrite: later accumulation must start from it
+        run(24, 8)
+        run(32, 8)
+        r.ctx.Finish()
+    ga, gb = a.result(), b.result()
+    a.close()
+    b.close()
+    assert ga.tobytes() == gb.tobytes(), f"{(ga != gb).any(axis=1).sum()} pixels differ"
