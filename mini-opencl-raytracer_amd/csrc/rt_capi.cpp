@@ -787,7 +787,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
     const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
-                        (k->sched == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0);
+                        (k->sched == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
+                        (k->sched == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math;

@@ -56,6 +56,13 @@ constexpr int kNumSched = 4;
 constexpr uint32_t kMaxFusedFrames = 8;
 // step schedule LDS per wave: the finish queue, 64 x {radiance, gid}
 constexpr uint32_t kFinishWaveBytes = 64u * 16u;
+#ifndef RT_RAY_RING
+#define RT_RAY_RING 1
+#endif
+// step schedule, LDS scenes: per-wave ring of camera rays generated a whole 8x8 tile at a time
+// ({dir, seed} + work-item id per slot)
+constexpr uint32_t kRingSlots = 64;
+constexpr uint32_t kRingWaveBytes = kRingSlots * 16u + kRingSlots * 4u;
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
 constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 

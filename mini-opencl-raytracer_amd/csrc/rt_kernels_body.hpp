@@ -74,16 +74,21 @@ struct Ray {
     uint32_t sgn;  // bit i = invDir[i] < 0
 };
 
-// kernel_bvh.cl:42-55
+// kernel_bvh.cl:42-55 after its normalize: invDir and sign of an already normalized direction
 template <class M>
-__device__ __forceinline__ Ray init_ray(F3 o, F3 d) {
+__device__ __forceinline__ Ray ray_from_unit(F3 o, F3 d) {
     Ray r;
-    d = normalize<M>(d);
     r.o = o;
     r.d = d;
     r.inv = F3{M::rcp(d.x), M::rcp(d.y), M::rcp(d.z)};
     r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
     return r;
+}
+
+// kernel_bvh.cl:42-55
+template <class M>
+__device__ __forceinline__ Ray init_ray(F3 o, F3 d) {
+    return ray_from_unit<M>(o, normalize<M>(d));
 }
 
 // kernel_bvh.cl:386-403
@@ -756,6 +761,21 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* fq = smem + lds_scene_f4<kLdsScene>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
     uint32_t fq_n = 0;  // wave-uniform
+#if RT_RAY_RING
+    // LDS scenes: per-wave ring of camera rays, generated one whole 8x8 tile (64 lanes) at a
+    // time and handed to idle lanes at refill -- create_ray then runs on full waves instead of
+    // on the few lanes a refill serves.  Same rays, same seeds, same pixel order.
+    constexpr bool kRing = kLdsScene;
+    float4* ring_d = smem + lds_scene_f4<kLdsScene>(a) + (fused ? 0u : 4u * kFinishSlots) +
+                     (uint32_t)(tid >> 6) * (kRingWaveBytes / 16u);
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + kRingSlots);
+#else
+    constexpr bool kRing = false;
+    float4* ring_d = nullptr;
+    uint32_t* ring_g = nullptr;
+#endif
+    uint32_t rc_head = 0, rc_n = 0;  // wave-uniform: ring entries [rc_head, rc_head + rc_n)
+    bool dry = false;                // wave-uniform: the work counter is exhausted
 
     LaneStats st;
     uint32_t state = kIdle;
@@ -820,7 +840,70 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 }
                 if (state == kDone) state = kIdle;
             }
-            while (!exhausted) {
+            while (kRing && !exhausted) {
+                const unsigned long long idle = __ballot(state == kIdle);
+                if (idle == 0ull) break;
+                if (rc_n == 0u) {
+                    if (!dry && chunk_used >= chunk_len) {
+                        if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail))
+                            dry = true;
+                        else
+                            chunk_used = 0;
+                    }
+                    if (dry) {
+                        exhausted = true;
+                        break;
+                    }
+                    // one 8x8 tile, one work item per lane (chunks are whole tiles)
+                    uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform
+                    const uint32_t slot = fused ? tile / a.nTiles : 0u;
+                    tile -= slot * a.nTiles;
+                    const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+                    const uint32_t x = tx * 8u + ((uint32_t)lane & 7u),
+                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + ((uint32_t)lane >> 3);
+                    const uint64_t g64 = (uint64_t)row * a.width + x;
+                    const bool valid = x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd;
+                    const unsigned long long vm = __ballot(valid);
+                    if (valid) {
+                        uint32_t sd = (uint32_t)g64 + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
+                        const Ray cr = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, sd);
+                        const uint32_t pos = lane_rank(vm);
+                        ring_d[pos] = make_float4(cr.d.x, cr.d.y, cr.d.z, __uint_as_float(sd));
+                        ring_g[pos] = (uint32_t)g64 + (fused ? slot * a.radStride : 0u);
+                    }
+                    rc_head = 0;
+                    rc_n = (uint32_t)__popcll(vm);
+                    chunk_used += 64u;
+                    continue;
+                }
+                const uint32_t rank = lane_rank(idle);
+                const uint32_t take = min((uint32_t)__popcll(idle), rc_n);
+                if (state == kIdle && rank < take) {
+                    const float4 e = ring_d[rc_head + rank];
+                    gid = ring_g[rc_head + rank];
+                    seed = __float_as_uint(e.w);
+                    ray = ray_from_unit<M>(camPos, F3{e.x, e.y, e.z});
+                    radiance = f3s(0.0f);
+                    beta = f3s(1.0f);
+                    bounce = 0;
+                    if (bounces > 0u) {
+                        state = kTrav;
+                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
+                        cur = 0;
+                        if (kStats) ++st.rays;
+                    } else {
+                        state = kDone;  // no bounce: radiance max(0, 0) = 0
+                        const uint32_t slot = fused ? gid / a.radStride : 0u;
+                        if (a.hitIds && slot + 1u == a.nFrames) {
+                            a.hitIds[gid - slot * a.radStride] = -1;
+                            a.hitT[gid - slot * a.radStride] = 0.0f;
+                        }
+                    }
+                }
+                rc_head += take;
+                rc_n -= take;
+            }
+            while (!kRing && !exhausted) {
                 const unsigned long long idle = __ballot(state == kIdle);
                 if (idle == 0ull) break;
                 if (chunk_used >= chunk_len) {
@@ -845,7 +928,18 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;
                         seed = gid + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
+#ifdef RT_CAM_TWICE
+                        const uint32_t seed_in = seed;
+#endif
                         ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
+#ifdef RT_CAM_TWICE
+                        {  // timing experiment only: the camera ray computed twice
+                            uint32_t s2 = seed_in ^ (a.poolShadeMin >> 7);
+                            const Ray r2 = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, s2);
+                            const float z = (float)(a.poolShadeMin >> 7);
+                            ray.d.x = ray.d.x + (r2.d.y * z + r2.d.z * z);
+                        }
+#endif
                         const bool last_frame = slot + 1u == a.nFrames;
                         if (fused) gid += slot * a.radStride;
                         radiance = f3s(0.0f);
