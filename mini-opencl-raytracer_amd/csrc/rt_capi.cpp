@@ -89,7 +89,10 @@ struct rt_kernel_s {
     float f3[3][4] = {};              // slots 11..13
     int math = RT_MATH_SHIPPED;  // the reference as its host builds it (rt_hip.h)
     int sched = RT_SCHED_STEP;
-    uint32_t refill_min = 8, shade_min = 48;   // step schedule thresholds (swept on MI355X)
+    // step schedule thresholds (lanes), swept on MI355X: LDS scenes (camera-ray ring)
+    // profiles/r01/threshold_sweep_ring.txt; scenes read from HBM/L2 keep 8 / 48
+    uint32_t refill_min = 6, shade_min = 44;
+    uint32_t refill_min_g = 8, shade_min_g = 48;
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
     uint32_t chunk_pixels = 128, tail_chunk = 64;  // pixels per work-counter fetch: bulk, tail
@@ -546,8 +549,10 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     rt_kernel k = new (std::nothrow) rt_kernel_s();
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
-    if (const char* v = std::getenv("RT_REFILL_MIN")) k->refill_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_SHADE_MIN")) k->shade_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_REFILL_MIN"))
+        k->refill_min = k->refill_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_SHADE_MIN"))
+        k->shade_min = k->shade_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_CHUNK"))
@@ -785,6 +790,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // (48 B per triangle, 64 B per material); no stack
     const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
+    a.refillMin = lds ? k->refill_min : k->refill_min_g;
+    a.shadeMin = lds ? k->shade_min : k->shade_min_g;
     a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
     const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
                         (k->sched == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
