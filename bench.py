@@ -45,7 +45,7 @@ CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
