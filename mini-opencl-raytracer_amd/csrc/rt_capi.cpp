@@ -100,7 +100,8 @@ struct rt_kernel_s {
                                                // (swept on MI355X: profiles/r01/chunk_sweep.txt)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
-    uint32_t* accum_key = nullptr;     // fused frames: sky-shortcut key state (4 words, zeroed once)
+    uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
+    int pf_parity = 0;                 // per-frame key slot read by the next launch
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
@@ -570,8 +571,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     }
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
-    if (e == hipSuccess) e = hipMalloc(&k->accum_key, 16);
-    if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 16, qs(ctx));
+    if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
+    if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
     if (e == hipSuccess) e = hipStreamSynchronize(qs(ctx));
     if (e != hipSuccess) {
@@ -782,6 +783,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.radBuf = k->rad_buf[rs];
         a.frameFlags = k->frame_flags[rs];
     }
+    if (n_frames == 1 && k->sched == RT_SCHED_STEP) {
+        a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
+        a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
+    }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
@@ -835,6 +840,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         (void)hipEventRecord(ev1, ctx->stream);
         k->pending_events.emplace_back(ev0, ev1);
     }
+    if (a.pfKeyIn) k->pf_parity ^= 1;
     if (n_frames > 1) {
         // fused frames: the gamma accumulation of every frame, in order, per pixel -- on the
         // accumulation stream after this render, overlapping whatever the main stream runs next

@@ -752,6 +752,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const uint32_t total = a.nTiles * 64u * (fused ? a.nFrames : 1u);
     // the radiance of a primary miss, max(1 * 0.5*skybox + 0, 0) per component (kernel_bvh.cl:360, :383)
     const float krad = M::max(madd<M>(1.0f, 0.5f * a.skyboxIntensity, 0.0f), 0.0f);
+    // per-frame launches: a finished path with radiance (K_rad, K_rad, K_rad) over a stored value
+    // of (K_old, K_old, K_old) gets gamma_out(frameCount, K_old, K_rad), computed once per wave
+    // here -- the same operations on the same bits as finish_color -- instead of 6 pow in the
+    // finish queue (56 % of the 16:9 Cornell view is sky).  Bit equality decides, so the key
+    // chain (launch to launch, pfKeyIn -> pfKeyOut) only affects how often the shortcut applies.
+    float k_old = 0.0f, k_out = 0.0f;
+    if (!fused && a.pfKeyIn) {
+        k_old = __uint_as_float(*a.pfKeyIn);
+        // three equal components; wave-uniform, kept in scalar registers
+        k_out = __uint_as_float(__builtin_amdgcn_readfirstlane(
+            __float_as_uint(gamma_out<M>(a.frameCount, f3s(k_old), f3s(krad)).x)));
+        if (blockIdx.x == 0 && tid == 0) *a.pfKeyOut = __float_as_uint(k_out);
+    }
     const uint32_t rowEnd = a.rowBegin + a.rowCount;
     const int lane = tid & 63;
     const uint32_t kRefillMin = a.refillMin;  // finish + refill when this many lanes are free
@@ -819,6 +832,22 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                                       __float_as_uint(radiance.z) == __float_as_uint(krad);
                     if (!skyv) a.radBuf[gid] = make_float4(radiance.x, radiance.y, radiance.z, 0.0f);
                     a.frameFlags[gid] = skyv ? 1u : 0u;
+                    state = kIdle;
+                }
+            }
+            if (!fused && a.pfKeyIn && state == kDone &&
+                __float_as_uint(radiance.x) == __float_as_uint(krad) &&
+                __float_as_uint(radiance.y) == __float_as_uint(krad) &&
+                __float_as_uint(radiance.z) == __float_as_uint(krad)) {
+                bool chain = a.frameCount == 0u;  // frame 0 ignores the stored value
+                if (!chain) {
+                    const float4 o = a.result[gid];
+                    chain = __float_as_uint(o.x) == __float_as_uint(k_old) &&
+                            __float_as_uint(o.y) == __float_as_uint(k_old) &&
+                            __float_as_uint(o.z) == __float_as_uint(k_old);
+                }
+                if (chain) {
+                    a.result[gid] = make_float4(k_out, k_out, k_out, 0.0f);
                     state = kIdle;
                 }
             }
