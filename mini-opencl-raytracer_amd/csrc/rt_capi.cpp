@@ -102,6 +102,7 @@ struct rt_kernel_s {
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
+    int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always (RT_PF_SKY)
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
@@ -554,6 +555,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
         k->refill_min = k->refill_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SHADE_MIN"))
         k->shade_min = k->shade_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_PF_SKY")) k->pf_sky = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_CHUNK"))
@@ -783,10 +785,6 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.radBuf = k->rad_buf[rs];
         a.frameFlags = k->frame_flags[rs];
     }
-    if (n_frames == 1 && k->sched == RT_SCHED_STEP) {
-        a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
-        a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
-    }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
@@ -823,6 +821,13 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                            : 0u;
     }
 
+    // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch
+    // start, which pays off from ~1k pixels per wave (4K) and not on small frames (512^2, 1080p)
+    if (n_frames == 1 && k->sched == RT_SCHED_STEP &&
+        (k->pf_sky == 2 || (k->pf_sky == 1 && g1 - g0 >= 1024u * 4u * grid))) {
+        a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
+        a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
+    }
     if (k->sched != RT_SCHED_TILES) {
         hipError_t me = hipMemsetAsync(k->work_counter, 0, 16, ctx->stream);
         if (me != hipSuccess) return map_hip(me);

@@ -282,3 +282,28 @@ def test_large_leaf_uses_global_layout(cornell, oracle_mod):
     assert np.array_equal(ids, wids)
     _assert_bits(rgb(got), rgb(want), "root-leaf radiance")
     assert (st["node_visits"], st["tri_tests"]) == (c["node_visits"], c["tri_tests"])
+
+
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_SHIPPED])
+def test_per_frame_sky_shortcut(cornell, oracle_mod, monkeypatch, math):
+    """Per-frame launches with the sky shortcut forced on (RT_PF_SKY=2; by default it is used
+    from ~1k pixels per wave): frames 1..6, then a frame with another skybox intensity (the key
+    chain no longer matches the stored sky values, so the bit check must fall back to the full
+    accumulation), then frames 8..9 -- bit-identical to the shortcut off and, pinned, to the oracle."""
+    W, H = 192, 96
+    seq = [(f, 1.0) for f in range(1, 7)] + [(7, 1.5)] + [(8, 1.5), (9, 1.0)]
+    outs = []
+    for mode in ("2", "0"):
+        monkeypatch.setenv("RT_PF_SKY", mode)
+        r = HipRenderer(cornell, W, H, math=math)
+        for f, sky in seq:
+            r.frame(f, light_bounces=3, skybox=sky)
+        outs.append(r.result())
+        r.close()
+    assert outs[0].tobytes() == outs[1].tobytes()
+    if math == N.MATH_PINNED:
+        res = np.zeros((W * H, 4), np.float32)
+        for f, sky in seq:
+            res, _, _, _ = oracle_mod.render(cornell, W, H, frame_count=f, light_bounces=3, skybox=sky,
+                                             result=res, threads=16)
+        _assert_bits(rgb(outs[0]), rgb(res), "per-frame sky shortcut vs oracle")
