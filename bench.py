@@ -204,32 +204,47 @@ def main():
         plans = [mg.pack_plan(r.W, r.H, world, q) for q in range(world)]
         if args.dist_backend == "nccl" and not args.no_overlap:
             # Pipelined: step k's staging buffer is gathered on RCCL's stream while step k+1
-            # renders on the kernel's stream; rank 0 unpacks step k into the final image
-            # after step k+1's frames are queued.  Two staging slots; every hand-off is a
-            # stream-side wait (no host sync), and the timed region ends with the last
-            # gather landed.
+            # renders on the kernel's stream; rank 0 unpacks step k into the final image on a
+            # side stream, so its render stream never carries the unpack copies (at N = 8 that
+            # is 7 x 16.6 MB per step that would otherwise make rank 0 the slowest).  Two
+            # staging slots; every hand-off is a stream-side event wait (no host sync), and
+            # the timed region ends with the last gather landed.
             dev = torch.device("cuda", device)
             ext = torch.cuda.ExternalStream(r.ctx.stream(), device=dev)
+            side = torch.cuda.Stream(device=dev)
             stages = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(2)]
             parts = [[torch.empty_like(stages[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
-            final = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16) if rank == 0 else None
+            final = torch.zeros(r.W * r.H * 4, dtype=torch.float32, device=dev) if rank == 0 else None
             pending = [None, None]
+            landed = [None, None]  # event on `side`: slot's gather (and unpack) done
             slot = [0]
+
+            def unpack(part, plan):
+                # mg.unpack_device as strided tensor copies (float32 elements: every offset and
+                # pitch is a multiple of 16 B)
+                for rc in plan:
+                    dst = final.as_strided((rc.rows, rc.width // 4), (rc.img_pitch // 4, 1), rc.img_offset // 4)
+                    src = part[rc.stage_offset // 4: rc.stage_offset // 4 + rc.rows * rc.width // 4]
+                    dst.copy_(src.view(rc.rows, rc.width // 4))
 
             def land(s):
                 if pending[s] is None:
                     return
-                with torch.cuda.stream(ext):
+                with torch.cuda.stream(side):
                     pending[s].wait()
-                if rank == 0:
-                    for q in range(world):
-                        mg.unpack_device(r.ctx, parts[s][q].data_ptr(), plans[q], final)
+                    if rank == 0:
+                        for q in range(world):
+                            unpack(parts[s][q], plans[q])
+                    landed[s] = torch.cuda.Event()
+                    landed[s].record(side)
                 pending[s] = None
 
             def gather():
                 s = slot[0]
                 slot[0] ^= 1
                 land(s ^ 1)
+                if landed[s] is not None:  # slot s's previous gather/unpack (a step ago) is done
+                    ext.wait_event(landed[s])
                 mg.pack_device(r.ctx, r.out, plans[rank], stages[s].data_ptr())
                 with torch.cuda.stream(ext):
                     pending[s] = dist.gather(stages[s], parts[s], dst=0, async_op=True)
@@ -339,7 +354,8 @@ def main():
         a = np.empty((r.H * r.W, 4), np.float32)
         b = np.empty_like(a)
         r.ctx.ReadBuffer(r.out, a)
-        r.ctx.ReadBuffer(final, b)
+        torch.cuda.synchronize()
+        b[:] = final.cpu().numpy().reshape(b.shape)  # the pipelined flow's final image (a tensor)
         rows = np.concatenate([np.arange(bb * mg.BAND_ROWS, min(r.H, (bb + 1) * mg.BAND_ROWS)) for bb in r.bands])
         a, b = a.reshape(r.H, r.W, 4)[rows], b.reshape(r.H, r.W, 4)[rows]
         if not (a.view(np.uint32) == b.view(np.uint32)).all():
