@@ -114,12 +114,21 @@ def bunny_proxy(max_prims_in_node: int = 4, path: str | None = None, cache: bool
     """Generate (if needed) and load the proxy through the product OBJ loader + SAH builder;
     the built arrays are kept in a binary scene cache next to the OBJ (rtsSaveScene)."""
     path = path or os.path.join(GEN_DIR, "bunny_proxy.obj")
+    # several ranks (bench.py --gpus N) may generate at once: write to a private temporary
+    # file and rename it into place, so a reader sees no file or a complete one
+    tag = f".{os.getpid()}.tmp"
     if not os.path.exists(path):
-        write_bunny_proxy(path)
+        tmp_dir = os.path.join(os.path.dirname(os.path.abspath(path)), "tmp" + tag)
+        tmp_obj = os.path.join(tmp_dir, os.path.basename(path))
+        write_bunny_proxy(tmp_obj)  # OBJ + MTL with their final names, in a private directory
+        os.replace(tmp_obj[:-4] + ".mtl", path[:-4] + ".mtl")
+        os.replace(tmp_obj, path)
+        os.rmdir(tmp_dir)
     cpath = f"{path[:-4]}.mp{max_prims_in_node}.rtscene"
     if cache and os.path.exists(cpath) and os.path.getmtime(cpath) >= os.path.getmtime(path):
         return load_scene(cpath, max_prims_in_node)
     sc = load_obj(path, max_prims_in_node)
     if cache:
-        save_scene(sc, cpath)
+        save_scene(sc, cpath + tag)
+        os.replace(cpath + tag, cpath)
     return sc
