@@ -102,6 +102,7 @@ struct rt_kernel_s {
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
+    int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major (RT_TILE_MAJOR)
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always (RT_PF_SKY)
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
@@ -555,6 +556,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
         k->refill_min = k->refill_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SHADE_MIN"))
         k->shade_min = k->shade_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_TILE_MAJOR")) k->tile_major = std::max(-1, std::min(1, std::atoi(v)));
     if (const char* v = std::getenv("RT_PF_SKY")) k->pf_sky = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
     if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
@@ -816,6 +818,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // bulk chunks only when every resident wave gets at least two of them; a small frame
         // (512x512: ~40 pixels per wave) is handed out 64 pixels at a time
         const uint64_t tot = (uint64_t)a.nTiles * 64u * n_frames, waves = grid * 4u;
+        // tile-major order for large fused launches on the HBM/L2 scene path: coherent fetches
+        // (bunny proxy, N = 1: -1.4 %); with few items per wave (multi-GPU ranks) it bunches a
+        // costly tile's frames into the tail, so frame-major there (work_order_ab.txt)
+        a.tileMajor = n_frames > 1 && (k->tile_major == 1 || (k->tile_major < 0 && !lds && tot >= 4096u * waves)) ? 1u : 0u;
         a.chunkSplit = tot >= 2u * waves * k->chunk_pixels
                            ? (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels)
                            : 0u;

@@ -45,6 +45,7 @@ struct KernelArgs {
     float4* radBuf;
     uint8_t* frameFlags;                // [slot * radStride + gid]: 1 = radiance (K_rad x3), not in radBuf
     uint32_t nFrames, radStride;
+    uint32_t tileMajor;                 // fused: work items ordered (tile, frame) instead of (frame, tile)
     // per-frame launches (step schedule): sky-pixel shortcut key, chained launch to launch --
     // pfKeyIn = the value all-sky pixels hold if they followed the chain, pfKeyOut = this launch's
     const uint32_t* pfKeyIn;

@@ -885,7 +885,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                     // one 8x8 tile, one work item per lane (chunks are whole tiles)
                     uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform
-                    const uint32_t slot = fused ? tile / a.nTiles : 0u;
+                    const uint32_t slot = fused ? tile / a.nTiles : 0u;  // frame-major (LDS scenes)
                     tile -= slot * a.nTiles;
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + ((uint32_t)lane & 7u),
@@ -948,8 +948,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 if (state == kIdle && rank < take) {
                     const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
                     uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                    const uint32_t slot = fused ? tile / a.nTiles : 0u;
-                    tile -= slot * a.nTiles;
+                    // fused work order: frame-major (all tiles of a frame, then the next: cheap
+                    // sky tiles and costly tiles mix in every wave), or -- large launches on
+                    // scenes read from HBM/L2 (a.tileMajor) -- tile-major, a tile's frames back
+                    // to back for coherent node and triangle fetches
+                    // (profiles/r01/work_order_ab.txt)
+                    uint32_t slot = 0;
+                    if (fused && a.tileMajor) {
+                        slot = tile % a.nFrames;
+                        tile /= a.nFrames;
+                    } else if (fused) {
+                        slot = tile / a.nTiles;
+                        tile -= slot * a.nTiles;
+                    }
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -957,18 +968,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;
                         seed = gid + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
-#ifdef RT_CAM_TWICE
-                        const uint32_t seed_in = seed;
-#endif
                         ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
-#ifdef RT_CAM_TWICE
-                        {  // timing experiment only: the camera ray computed twice
-                            uint32_t s2 = seed_in ^ (a.poolShadeMin >> 7);
-                            const Ray r2 = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, s2);
-                            const float z = (float)(a.poolShadeMin >> 7);
-                            ray.d.x = ray.d.x + (r2.d.y * z + r2.d.z * z);
-                        }
-#endif
                         const bool last_frame = slot + 1u == a.nFrames;
                         if (fused) gid += slot * a.radStride;
                         radiance = f3s(0.0f);

@@ -145,3 +145,13 @@ def test_overlapped_accumulation_stays_in_order(cornell):
     a.close()
     b.close()
     assert ga.tobytes() == gb.tobytes(), f"{(ga != gb).any(axis=1).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("force_global", [False, True])
+def test_fused_tile_major_order(cornell, monkeypatch, force_global):
+    """Tile-major work order (RT_TILE_MAJOR=1; chosen automatically for large launches on the
+    HBM/L2 scene path): the frames of a tile back to back -- same bits as per-frame launches."""
+    monkeypatch.setenv("RT_TILE_MAJOR", "1")
+    W, H = 248, 136
+    _same(_render(cornell, W, H, 2, 7, True, force_global=force_global, interleave=(2, 1)),
+          _render(cornell, W, H, 2, 7, False, force_global=force_global, interleave=(2, 1)))
