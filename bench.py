@@ -46,6 +46,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--pack-stream", choices=["accum", "main"], default="accum",
+                   help="pipelined RCCL gather: pack each step's bands on the accumulation stream "
+                        "(the next render does not wait for the accumulation) or on the main stream")
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
@@ -209,8 +212,14 @@ def main():
             # is 7 x 16.6 MB per step that would otherwise make rank 0 the slowest).  Two
             # staging slots; every hand-off is a stream-side event wait (no host sync), and
             # the timed region ends with the last gather landed.
+            # The pack of step k runs on the context's accumulation stream right after step k's
+            # accumulation (rtContextSetReadbackOnAccumStream), so the kernel stream goes straight
+            # on to step k+1's render and the accumulation keeps overlapping it at N > 1 too; the
+            # gather is issued from its own stream after the pack.
             dev = torch.device("cuda", device)
-            ext = torch.cuda.ExternalStream(r.ctx.stream(), device=dev)
+            r.ctx.set_readback_on_accum_stream(args.pack_stream == "accum")
+            acc = torch.cuda.ExternalStream(r.ctx.accum_stream(), device=dev)
+            issue = torch.cuda.Stream(device=dev)
             side = torch.cuda.Stream(device=dev)
             stages = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(2)]
             parts = [[torch.empty_like(stages[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
@@ -244,9 +253,10 @@ def main():
                 slot[0] ^= 1
                 land(s ^ 1)
                 if landed[s] is not None:  # slot s's previous gather/unpack (a step ago) is done
-                    ext.wait_event(landed[s])
-                mg.pack_device(r.ctx, r.out, plans[rank], stages[s].data_ptr())
-                with torch.cuda.stream(ext):
+                    acc.wait_event(landed[s])
+                mg.pack_device(r.ctx, r.out, plans[rank], stages[s].data_ptr())  # on `acc`
+                issue.wait_stream(acc)
+                with torch.cuda.stream(issue):
                     pending[s] = dist.gather(stages[s], parts[s], dst=0, async_op=True)
 
             def land_all():

@@ -209,6 +209,14 @@ int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem src, size_t offset, size
 int rtBufferGetDevicePointer(rt_mem mem, void** dptr);
 int rtBufferGetSize(rt_mem mem, size_t* size);
 int rtContextGetStream(rt_context ctx, void** hip_stream);
+/* Extension (multi-GPU gather): with `enable`, rtEnqueueCopyBufferRectToPointer runs on the
+ * context's accumulation stream, right after the fused-frame accumulations enqueued so far
+ * and before later ones, instead of joining them into the main stream -- so the next fused
+ * render is not held up by the read-back.  Work that consumes the copied bytes waits on the
+ * stream rtContextGetAccumStream returns (e.g. an event recorded there after the copies);
+ * later calls on the context stay ordered after the copies as before. */
+int rtContextSetReadbackOnAccumStream(rt_context ctx, int enable);
+int rtContextGetAccumStream(rt_context ctx, void** hip_stream);
 int rtContextGetDevice(rt_context ctx, int* device_index);
 
 /* Library identification (for smoke checks): returns a static string. */

@@ -116,6 +116,8 @@ _HIP_PROTOS = {
     "rtBufferGetDevicePointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "rtBufferGetSize": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
     "rtContextGetStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "rtContextSetReadbackOnAccumStream": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtContextGetAccumStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "rtContextGetDevice": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "rtGetBuildInfo": (ctypes.c_char_p, []),
 }

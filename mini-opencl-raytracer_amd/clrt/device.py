@@ -86,6 +86,15 @@ class CLContext:
         check(self._lib.rtContextGetStream(self.handle, ctypes.byref(s)), "stream")
         return int(s.value or 0)
 
+    def accum_stream(self) -> int:
+        """The fused-frame accumulation stream (rtContextGetAccumStream)."""
+        s = ctypes.c_void_p()
+        check(self._lib.rtContextGetAccumStream(self.handle, ctypes.byref(s)), "accumulation stream")
+        return int(s.value or 0)
+
+    def set_readback_on_accum_stream(self, enable: bool) -> None:
+        check(self._lib.rtContextSetReadbackOnAccumStream(self.handle, int(bool(enable))), "readback stream")
+
     def release(self) -> None:
         if self.handle:
             self._lib.rtReleaseContext(self.handle)

@@ -58,6 +58,9 @@ struct rt_context_s {
     hipEvent_t atail = nullptr;  // last accumulation enqueued on astream
     bool apending = false;
     bool overlap = true;  // RT_ACCUM_OVERLAP=0: accumulate on the main stream
+    // rtContextSetReadbackOnAccumStream: buffer -> pointer rect copies go to astream, right after
+    // the accumulation they read, so the main stream runs on into the next render
+    bool readback_on_astream = false;
 };
 
 namespace {
@@ -991,8 +994,31 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
     if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
     if (src_offset + (rows - 1) * src_pitch + width_bytes > src->size) return RT_INVALID_VALUE;
+    if (ctx->readback_on_astream && ctx->overlap) {
+        // after every accumulation enqueued so far, before any later one (astream is in order);
+        // later main-stream work that joins (qs) waits for the copy too
+        hipError_t e = hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
+                                        width_bytes, rows, hipMemcpyDeviceToDevice, ctx->astream);
+        if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
+        if (e == hipSuccess) ctx->apending = true;
+        return map_hip(e);
+    }
     return map_hip(hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
                                     width_bytes, rows, hipMemcpyDeviceToDevice, qs(ctx)));
+}
+
+int rtContextSetReadbackOnAccumStream(rt_context ctx, int enable) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    ctx->readback_on_astream = enable != 0;
+    return RT_SUCCESS;
+}
+
+int rtContextGetAccumStream(rt_context ctx, void** s) {
+    if (!ctx) return RT_INVALID_CONTEXT;
+    if (!s) return RT_INVALID_VALUE;
+    *s = ctx->overlap ? ctx->astream : qs(ctx);
+    return RT_SUCCESS;
 }
 
 int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src_pitch, rt_mem dst,
