@@ -155,3 +155,30 @@ def test_fused_tile_major_order(cornell, monkeypatch, force_global):
     W, H = 248, 136
     _same(_render(cornell, W, H, 2, 7, True, force_global=force_global, interleave=(2, 1)),
           _render(cornell, W, H, 2, 7, False, force_global=force_global, interleave=(2, 1)))
+
+
+def test_readback_on_accum_stream(cornell):
+    """rtContextSetReadbackOnAccumStream: a rect copy of the output queued after a fused launch
+    runs right after that launch's accumulation on the accumulation stream, so it holds that
+    step's image even though the next fused launch is queued before anything waits for it."""
+    import torch
+    torch.zeros(1, device="cuda:0")  # torch's HIP context before the library's
+    W, H = 224, 128
+    r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    r.ctx.set_readback_on_accum_stream(True)
+    dst = torch.empty(W * H * 4, dtype=torch.float32, device="cuda:0")
+    r.frame(1, n_frames=8, light_bounces=9)
+    r.ctx.CopyRectToDevicePointer(r.out, 0, W * 16, W * 16, H, dst.data_ptr(), W * 16)
+    r.frame(9, n_frames=8, light_bounces=9)
+    torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(r.ctx.accum_stream()))
+    step1 = dst.cpu().numpy().reshape(W * H, 4)
+    step2 = r.result()
+    r.close()
+    ref = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    ref.frame(1, n_frames=8, light_bounces=9)
+    want1 = ref.result()
+    ref.frame(9, n_frames=8, light_bounces=9)
+    want2 = ref.result()
+    ref.close()
+    assert step1.tobytes() == want1.tobytes()
+    assert step2.tobytes() == want2.tobytes()
