@@ -738,6 +738,10 @@ __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__pop
 template <class M, bool kLdsScene, bool kStats>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
+    // scenes read from HBM/L2: the render's waves issue ahead of co-resident accumulation waves
+    // (second stream), which then only fill the slots the render leaves idle (bunny proxy -1.5 %;
+    // on the VALU-bound LDS path it costs 0.8 %: profiles/r01/render_priority_ab.txt)
+    if (!kLdsScene) __builtin_amdgcn_s_setprio(1);
     const SceneView sc = stage_scene<kLdsScene>(a);
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
