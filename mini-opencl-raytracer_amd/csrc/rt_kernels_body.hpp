@@ -713,6 +713,9 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 }
 // steps of the chosen kind per scheduling decision (thresholds are re-checked after each
 // burst): the per-step ballots and threshold tests cost about as much as a node visit
+#ifndef RT_GPHASE
+#define RT_GPHASE 1  // global path: phase priorities (traversal 3 / shading 1) instead of a fixed 1
+#endif
 #ifndef RT_NODE_BURST
 #define RT_NODE_BURST 6
 #endif
@@ -740,7 +743,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
     // scenes read from HBM/L2: the render's waves issue ahead of co-resident accumulation waves
     // (second stream), which then only fill the slots the render leaves idle (bunny proxy -1.5 %;
-    // on the VALU-bound LDS path it costs 0.8 %: profiles/r01/render_priority_ab.txt)
+    // profiles/r01/render_priority_ab.txt); traversal steps raise it further (below)
     if (!kLdsScene) __builtin_amdgcn_s_setprio(1);
     const SceneView sc = stage_scene<kLdsScene>(a);
 
@@ -1006,6 +1009,10 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         }
 
         // ---- traversal steps -----------------------------------------------------------------
+        // wave priority by phase: traversal steps (short dependent LDS/VALU chains) issue ahead
+        // of waves that shade or refill (long independent VALU runs), which fill the gaps
+        // (profiles/r01/phase_priority_ab.txt)
+        if (kLdsScene || RT_GPHASE) __builtin_amdgcn_s_setprio(3);
         // Each step is wave-uniform: either a node step (TRAV lanes visit one node) or a
         // triangle step (LEAF lanes test one triangle), chosen by which serves more lanes per
         // instruction (weights ~ the two bodies' VALU cost), so the wave never pays both
@@ -1075,6 +1082,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         }
 
         // ---- shading ---------------------------------------------------------------------------
+        if (kLdsScene) __builtin_amdgcn_s_setprio(0);
+        else if (RT_GPHASE) __builtin_amdgcn_s_setprio(1);
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
         if (kStats) {
             cyc_trav += tC - tB;
