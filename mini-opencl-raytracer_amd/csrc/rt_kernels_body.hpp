@@ -713,6 +713,12 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 }
 // steps of the chosen kind per scheduling decision (thresholds are re-checked after each
 // burst): the per-step ballots and threshold tests cost about as much as a node visit
+#ifndef RT_PRIO_SHADE
+#define RT_PRIO_SHADE 1  // LDS path: wave priority while shading (traversal steps run at 3)
+#endif
+#ifndef RT_PRIO_REFILL
+#define RT_PRIO_REFILL -1  // LDS path: wave priority during finish + refill (-1: as shading left it)
+#endif
 #ifndef RT_GPHASE
 #define RT_GPHASE 1  // global path: phase priorities (traversal 3 / shading 1) instead of a fixed 1
 #endif
@@ -822,6 +828,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 
     for (;;) {
         // ---- finish + refill: accumulate finished paths, start new pixels ----------------------
+        if (kLdsScene && RT_PRIO_REFILL >= 0) __builtin_amdgcn_s_setprio(RT_PRIO_REFILL);
         uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t n_free = popc_ballot(state == kIdle || state == kDone);
         if (n_free == 64u || (!exhausted && n_free >= kRefillMin)) {
@@ -1082,7 +1089,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         }
 
         // ---- shading ---------------------------------------------------------------------------
-        if (kLdsScene) __builtin_amdgcn_s_setprio(0);
+        if (kLdsScene) __builtin_amdgcn_s_setprio(RT_PRIO_SHADE);
         else if (RT_GPHASE) __builtin_amdgcn_s_setprio(1);
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
         if (kStats) {
