@@ -1,28 +1,40 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s + ms/frame, 3840x2160 Cornell box, 8 spp path trace (BASELINE.json).
 
-One *step* = one full 8-spp render of the workload: KernelEntry launched for frames
-1..8 (9 light bounces, the reference defaults) into one accumulation buffer, then -- for
-N > 1 -- the per-rank row tiles gathered to rank 0 over RCCL (torch.distributed "nccl").
-Scene and output stay resident in HBM; nothing is read back to the host inside the
-timed region.
+One *step* = one full 8-spp render of the workload: KernelEntry for frames 1..8 (9 light
+bounces, the reference defaults) accumulated into one output buffer, then -- for N > 1 --
+every rank's interleaved 8-row bands gathered to rank 0 over RCCL by the library
+(rtCommEnqueueGatherBands, csrc/rt_comm.cpp).  Scene and output stay resident in HBM; nothing
+is read back to the host inside the timed region.  The process never imports torch: the only
+HIP runtime in it is the one librt_hip.so links (/opt/rocm).
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...; the
+  launcher only starts the processes -- ranks meet through the library's RCCL communicator)
 
 Rays are counted as the reference's Intersect() calls over all bounces and frames
-(SURVEY.md 8(d)); the count comes from an instrumented pass before the timed region and
-is deterministic (the HIP path is bit-exact with the oracle, tests/test_gpu_parity.py).
+(SURVEY.md 8(d)); the count comes from an instrumented pass before the timed region and is
+deterministic (the HIP path is bit-exact with the reference, tests/).
 
-Roofline: the dominant kernel is KernelEntry.  achieved = algorithmic bytes per launch
-(48*node_visits + 48*tri_tests + 164*hits + 32*W*H) / average launch
-duration from HIP events recorded on the kernel's own stream during the timed region;
-peak = 8000 GB/s (MI355X HBM3E).  traffic = HBM bytes per launch from rocprofv3 PMC
-counters (profiles/traffic.json, written by scripts/profile.sh) when present.
-cpu_baseline: the CPU oracle (a C restatement of kernel_bvh.cl) on the host cores, rank 0,
-N = 1 only, on a bounded sample (frames 1-2 of the same 4K render).
+Roofline of the dominant kernel (KernelEntry's render launch), per launch:
+  * bound "valu": the kernel is VALU-issue bound (the Cornell scene lives in LDS; HBM sees the
+    output only).  achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU of the
+    same command and build, profiles/pmc.json) / the launch's duration measured live here with
+    HIP events on the kernel's stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+    instruction (MI355X_MICROARCH.md).  frac = achieved / peak.
+  * lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU): active lanes per issued VALU op.
+  * traffic / hbm_frac: measured HBM bytes per launch ((2 FETCH_SIZE + WRITE_SIZE) KiB, the
+    guide's gfx950 correction) and their rate against 8 TB/s.
+  * alg_bytes_per_launch / alg_gbs: SURVEY 8(d)'s algorithmic bytes (48 B per node visit and
+    triangle test, 164 B per closest hit, 32 B output RMW per pixel) -- a plain number: most of
+    those bytes are LDS reads, not HBM traffic.
+cpu_baseline: the reference kernel itself (kernel_bvh.cl compiled unmodified for x86-64,
+oracle/_ref/libref_cpu.so) over all 8 frames of the same render on the host cores, rank 0,
+N = 1 only.
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -38,17 +50,16 @@ from clrt import _native as N  # noqa: E402
 from clrt import multigpu as mg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
-SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMD-32
+SIMDS = 256 * 4                    # MI355X: 256 CUs x 4 SIMD-32
+VALU_PEAK = SIMDS * 2.4e9 / 2.0    # wave64 VALU instructions per second (2 cycles each)
 CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+PMC_PATH = os.path.join(REPO, "profiles", "pmc.json")
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--pack-stream", choices=["accum", "main"], default="accum",
-                   help="pipelined RCCL gather: pack each step's bands on the accumulation stream "
-                        "(the next render does not wait for the accumulation) or on the main stream")
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--width", type=int, default=3840)
     p.add_argument("--height", type=int, default=2160)
@@ -67,68 +78,82 @@ def parse():
                    help="fused: the F frames of a step as one rtEnqueueKernelFrames call (one step launch "
                         "over (frame, pixel) work items + the per-pixel accumulation); per-frame: one "
                         "rtEnqueueKernel per frame, as the reference's RenderFrame loop. Same bits.")
+    p.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                   help="rtKernelSetTuning parameter (clrt._native.TUNING names); results unchanged")
+    p.add_argument("--no-accum-overlap", action="store_true",
+                   help="fused frames: accumulate on the main stream (rtContextSetAccumOverlap 0)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--no-overlap", action="store_true",
-                   help="N>1 nccl: gather after each step with a host sync instead of pipelining it")
+    p.add_argument("--gather-sync", action="store_true",
+                   help="N>1: wait for each step's gather before queueing the next step (no pipelining)")
     p.add_argument("--force-dist", action="store_true",
-                   help="run the N>1 flow even at WORLD_SIZE 1 (exercises the RCCL path on one GPU)")
+                   help="run the N>1 flow (RCCL communicator + gather) even at WORLD_SIZE 1")
     p.add_argument("--check-gather", action="store_true",
-                   help="after timing, check rank 0's bands in the gathered image (pipelined nccl)")
-    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
-                   help="gloo = dry run of the N>1 flow (host-staged gather; ranks may share a GPU)")
+                   help="after timing, rank 0 renders the whole frame unsharded and checks the gathered "
+                        "image against it byte for byte")
     return p.parse_args()
 
 
 class Rank:
-    """One GPU's share of the image: the interleaved 8-row bands b % world == rank
-    (clrt.multigpu), rendered at their global positions (global seeds)."""
+    """One GPU's share of the image: the interleaved 8-row bands b % world == rank, rendered
+    at their global positions (global seeds)."""
 
-    def __init__(self, scene, args, device, rank, world):
+    def __init__(self, scene, args, device, comm=None):
         self.args = args
         W, H = args.width, args.height
         self.W, self.H = W, H
-        self.rank, self.world = rank, world
+        self.ctx = comm.ctx if comm is not None else clrt.CLContext(device)
+        world, rank = (comm.nranks, comm.rank) if comm is not None else (1, 0)
         self.bands = mg.rank_bands(H, world, rank)
         self.pixels = sum(min(H, (b + 1) * mg.BAND_ROWS) - b * mg.BAND_ROWS for b in self.bands) * W
-        self.ctx = clrt.CLContext(device)
-        self.k = clrt.CLKernel(self.ctx, "KernelEntry")
         flags = N.MEM_READ_ONLY | N.MEM_COPY_HOST_PTR
         self.bufs = [self.ctx.create_buffer(flags, a.nbytes, a)
                      for a in (scene.triangles, scene.nodes, scene.materials)]
         self.out = self.ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
-        k = self.k
-        k.set_buffer(N.BUFFER_OUT, self.out)
-        k.set_buffer(N.BUFFER_SCENE, self.bufs[0])
-        k.set_buffer(N.BUFFER_NODE, self.bufs[1])
-        k.set_buffer(N.BUFFER_MATERIAL, self.bufs[2])
-        k.set_int(N.WIDTH, W)
-        k.set_int(N.HEIGHT, H)
-        k.set_uint(N.FRAME_SEED, 0)
-        k.set_int(N.LIGHT_BOUNCES, args.bounces)
-        k.set_int(N.LIGHT_TYPE, 0)
-        k.set_float(N.SKYBOX_INTENSITY, 1.0)
-        k.set_float3(N.CAMERA_POS, CAMERA[0])
-        k.set_float3(N.CAMERA_FRONT, CAMERA[1])
-        k.set_float3(N.CAMERA_UP, CAMERA[2])
-        k.set_math_mode({"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[args.math])
-        k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
-                        "pool": N.SCHED_POOL}[args.sched])
-        k.set_row_interleave(world, rank)
+        self.k = make_kernel(self.ctx, self.bufs, self.out, args)
+        if comm is not None:
+            comm.shard(self.k)
+        if args.no_accum_overlap:
+            self.ctx.set_accum_overlap(False)
 
-    def render(self):
+    def render(self, k=None):
         """frames 1..F accumulated (RenderFrame's m_FrameCount sequence): one launch per frame,
         or (--launch fused, default) one rtEnqueueKernelFrames call -- the same bits."""
+        k = k or self.k
         if self.args.launch == "fused":
-            self.k.set_uint(N.FRAME_COUNT, 1)
-            self.ctx.ExecuteKernelFrames(self.k, self.W * self.H, self.args.frames)
+            k.set_uint(N.FRAME_COUNT, 1)
+            self.ctx.ExecuteKernelFrames(k, self.W * self.H, self.args.frames)
             return
         for f in range(1, self.args.frames + 1):
-            self.k.set_uint(N.FRAME_COUNT, f)
-            self.ctx.ExecuteKernel(self.k, self.W * self.H)
+            k.set_uint(N.FRAME_COUNT, f)
+            self.ctx.ExecuteKernel(k, self.W * self.H)
 
     def finish(self):
         self.ctx.Finish()
+
+
+def make_kernel(ctx, bufs, out, args):
+    k = clrt.CLKernel(ctx, "KernelEntry")
+    k.set_buffer(N.BUFFER_OUT, out)
+    k.set_buffer(N.BUFFER_SCENE, bufs[0])
+    k.set_buffer(N.BUFFER_NODE, bufs[1])
+    k.set_buffer(N.BUFFER_MATERIAL, bufs[2])
+    k.set_int(N.WIDTH, args.width)
+    k.set_int(N.HEIGHT, args.height)
+    k.set_uint(N.FRAME_SEED, 0)
+    k.set_int(N.LIGHT_BOUNCES, args.bounces)
+    k.set_int(N.LIGHT_TYPE, 0)
+    k.set_float(N.SKYBOX_INTENSITY, 1.0)
+    k.set_float3(N.CAMERA_POS, CAMERA[0])
+    k.set_float3(N.CAMERA_FRONT, CAMERA[1])
+    k.set_float3(N.CAMERA_UP, CAMERA[2])
+    k.set_math_mode({"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[args.math])
+    k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
+                    "pool": N.SCHED_POOL}[args.sched])
+    for t in args.tune:
+        name, value = t.split("=", 1)
+        k.set_tuning(name, int(value))
+    return k
 
 
 def count_pass(r):
@@ -142,23 +167,87 @@ def count_pass(r):
     return s
 
 
-def cpu_baseline(scene, args):
+def kernel_source_hash() -> str:
+    """Hash of everything that shapes the render kernel's instruction stream: the PMC numbers in
+    profiles/pmc.json are only valid for the build they were measured on."""
+    h = hashlib.sha1()
+    files = sorted(glob.glob(os.path.join(REPO, "mini-opencl-raytracer_amd", "csrc", "rt_kernels*"))
+                   + [os.path.join(REPO, "mini-opencl-raytracer_amd", "csrc", "rt_math.hpp"),
+                      os.path.join(REPO, "include", "rt_pinned_math.h"),
+                      os.path.join(REPO, "include", "rt_cl_types.h"),
+                      os.path.join(REPO, "mini-opencl-raytracer_amd", "Makefile")])
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def workload_key(args, world, frames_per_launch):
+    return (f"{args.scene}_{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_{args.sched}_n{world}"
+            + ("_fused" if frames_per_launch > 1 else ""))
+
+
+def pinned_rays(r, args):
+    """Intersect() calls of the step under the pinned builtins -- exactly the CPU reference
+    build's count (HIP pinned == C oracle == kernel_bvh.cl on the CPU, bit for bit and counter
+    for counter: tests/test_gpu_parity.py, tests/test_ref_cpu.py)."""
+    k = make_kernel(r.ctx, r.bufs, r.out, args)
+    k.set_math_mode(N.MATH_PINNED)
+    k.set_stats(True)
+    r.render(k)
+    r.finish()
+    rays = k.stats()["rays"]
+    k.release()
+    return rays
+
+
+def cpu_baseline(scene, args, rays_per_step):
+    """The reference kernel (kernel_bvh.cl, compiled for x86-64) over all frames of the step;
+    rays_per_step: the pinned-math count of the same render."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle
+    import refcpu
     W, H = args.width, args.height
     threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
     res = np.zeros((W * H, 4), np.float32)
-    rays = 0
     t0 = time.perf_counter()
-    sample_frames = 2
-    for f in range(1, sample_frames + 1):
-        res, _, _, c = oracle.render(scene, W, H, frame_count=f, light_bounces=args.bounces, result=res,
-                                     threads=threads)
-        rays += c["rays"]
+    for f in range(1, args.frames + 1):
+        refcpu.render(scene, W, H, frame_count=f, light_bounces=args.bounces, result=res, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"frames 1-{sample_frames} of the same {W}x{H} {args.bounces}-bounce render, all pixels "
-                      f"({rays} rays, {dt:.2f} s wall)"}
+    return {"value": rays_per_step / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "reference",
+            "sample": f"the whole step: frames 1-{args.frames} of the {W}x{H} {args.bounces}-bounce render, "
+                      f"/root/reference/kernel_bvh.cl compiled unmodified for x86-64 (pinned builtins), "
+                      f"{threads} threads ({int(rays_per_step)} rays, {dt:.2f} s wall)",
+            "ms_per_frame": dt * 1e3 / args.frames}
+
+
+def roofline(args, world, frames_per_launch, kernel_ms, local_counts, tile_px):
+    alg_bytes = ((48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames
+                 + 32 * tile_px) * frames_per_launch
+    rl = {"bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "VALU wave-instructions/s",
+          "frac": None, "traffic": None, "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
+          "frames_per_launch": frames_per_launch, "lane_util": None, "hbm_frac": None,
+          "alg_bytes_per_launch": int(alg_bytes),
+          "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 2) if kernel_ms > 0 else None,
+          "pmc": None}
+    key = workload_key(args, world, frames_per_launch)
+    db = json.load(open(PMC_PATH)) if os.path.exists(PMC_PATH) else {}
+    e = db.get(key)
+    if e is None or kernel_ms <= 0:
+        rl["pmc"] = f"no PMC pass for {key} in profiles/pmc.json"
+        return rl
+    src = kernel_source_hash()
+    insts = e["SQ_INSTS_VALU"]
+    achieved = insts / (kernel_ms * 1e-3)
+    rl["achieved"] = round(achieved, 1)
+    rl["frac"] = round(achieved / VALU_PEAK, 4)
+    rl["lane_util"] = round(e["SQ_THREAD_CYCLES_VALU"] / (64.0 * insts), 4) if "SQ_THREAD_CYCLES_VALU" in e else None
+    if "hbm_bytes_per_launch" in e:
+        rl["traffic"] = int(e["hbm_bytes_per_launch"])
+        rl["hbm_frac"] = round(e["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    rl["pmc"] = {"file": "profiles/pmc.json", "key": key, "valu_insts_per_launch": int(insts),
+                 "kernel_ms_in_pmc_pass": e.get("kernel_ms"), "source_hash": e.get("source_hash"),
+                 "stale": e.get("source_hash") != src}
+    return rl
 
 
 def main():
@@ -166,19 +255,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    device = local
-    if world > 1 or args.force_dist:
-        import torch
-        import torch.distributed as dist_mod
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            device = local % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(device)
-            dist_mod.init_process_group("gloo")
-        dist = dist_mod
 
     if args.scene == "bunny":
         from clrt import proxy as clrt_proxy
@@ -192,188 +268,85 @@ def main():
         else:
             z = np.load(clrt.scene.CORNELL_NPZ, allow_pickle=False)
             ft, fm = z["triangles"].view(N.TRIANGLE_DTYPE), z["materials"].view(N.MATERIAL_DTYPE)
-        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=device)
-    r = Rank(scene, args, device, rank, world)
+        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=local)
+
+    comm = None
+    if world > 1 or args.force_dist:
+        # one rank per GPU: rank 0's RCCL id reaches the others through a file on this node
+        ctx = clrt.CLContext(local)
+        uid = mg.file_rendezvous(rank, world, mg.Comm.unique_id)
+        comm = mg.Comm.init_rank(ctx, world, uid, rank)
+        mg.Comm.barrier([comm])
+        if rank == 0:
+            mg.rendezvous_cleanup()
+    r = Rank(scene, args, local, comm)
 
     # instrumented pass: ray / node / triangle / hit counts of one step on this rank
     st = count_pass(r)
-    counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
-
-    gather = land_all = None
-    final = None
-    if dist is not None:
-        import torch
-        nbytes = mg.staging_bytes(r.W, r.H, world)
-        plans = [mg.pack_plan(r.W, r.H, world, q) for q in range(world)]
-        if args.dist_backend == "nccl" and not args.no_overlap:
-            # Pipelined: step k's staging buffer is gathered on RCCL's stream while step k+1
-            # renders on the kernel's stream; rank 0 unpacks step k into the final image on a
-            # side stream, so its render stream never carries the unpack copies (at N = 8 that
-            # is 7 x 16.6 MB per step that would otherwise make rank 0 the slowest).  Two
-            # staging slots; every hand-off is a stream-side event wait (no host sync), and
-            # the timed region ends with the last gather landed.
-            # The pack of step k runs on the context's accumulation stream right after step k's
-            # accumulation (rtContextSetReadbackOnAccumStream), so the kernel stream goes straight
-            # on to step k+1's render and the accumulation keeps overlapping it at N > 1 too; the
-            # gather is issued from its own stream after the pack.
-            dev = torch.device("cuda", device)
-            r.ctx.set_readback_on_accum_stream(args.pack_stream == "accum")
-            acc = torch.cuda.ExternalStream(r.ctx.accum_stream(), device=dev)
-            issue = torch.cuda.Stream(device=dev)
-            side = torch.cuda.Stream(device=dev)
-            stages = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(2)]
-            parts = [[torch.empty_like(stages[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
-            final = torch.zeros(r.W * r.H * 4, dtype=torch.float32, device=dev) if rank == 0 else None
-            pending = [None, None]
-            landed = [None, None]  # event on `side`: slot's gather (and unpack) done
-            slot = [0]
-
-            def unpack(part, plan):
-                # mg.unpack_device as strided tensor copies (float32 elements: every offset and
-                # pitch is a multiple of 16 B)
-                for rc in plan:
-                    dst = final.as_strided((rc.rows, rc.width // 4), (rc.img_pitch // 4, 1), rc.img_offset // 4)
-                    src = part[rc.stage_offset // 4: rc.stage_offset // 4 + rc.rows * rc.width // 4]
-                    dst.copy_(src.view(rc.rows, rc.width // 4))
-
-            def land(s):
-                if pending[s] is None:
-                    return
-                with torch.cuda.stream(side):
-                    pending[s].wait()
-                    if rank == 0:
-                        for q in range(world):
-                            unpack(parts[s][q], plans[q])
-                    landed[s] = torch.cuda.Event()
-                    landed[s].record(side)
-                pending[s] = None
-
-            def gather():
-                s = slot[0]
-                slot[0] ^= 1
-                land(s ^ 1)
-                if landed[s] is not None:  # slot s's previous gather/unpack (a step ago) is done
-                    acc.wait_event(landed[s])
-                mg.pack_device(r.ctx, r.out, plans[rank], stages[s].data_ptr())  # on `acc`
-                issue.wait_stream(acc)
-                with torch.cuda.stream(issue):
-                    pending[s] = dist.gather(stages[s], parts[s], dst=0, async_op=True)
-
-            def land_all():
-                land(0)
-                land(1)
-        else:
-            stage = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{device}")
-            host_staged = args.dist_backend == "gloo"
-
-            def gather():
-                # pack this rank's bands (2-D device copy on the kernel's stream), gather the
-                # staging buffers to rank 0, unpack them into rank 0's image
-                mg.pack_device(r.ctx, r.out, plans[rank], stage.data_ptr())
-                r.finish()
-                parts = mg.gather_to_root(dist, stage.cpu() if host_staged else stage, rank, world)
-                if rank == 0:
-                    if host_staged:
-                        parts = [p.to(stage.device) for p in parts]
-                    torch.cuda.current_stream().synchronize()
-                    for q in range(1, world):
-                        mg.unpack_device(r.ctx, parts[q].data_ptr(), plans[q], r.out)
-                    r.finish()
-
-        small_dev = f"cuda:{device}" if args.dist_backend == "nccl" else "cpu"
-        tot = torch.tensor(counts, dtype=torch.float64, device=small_dev)
-        dist.all_reduce(tot)
-        counts = tot.cpu().numpy()
+    local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
+    counts = local_counts
+    if comm is not None:
+        counts = mg.Comm.allreduce([comm], local_counts, N.COMM_SUM)[0]
 
     def step():
-        r.render()  # N = 1: steps are queued back to back (sync only around the timed region)
-        if gather is not None:
-            gather()
-
-    def steps(n):
-        for _ in range(n):
-            step()
-        if land_all is not None:
-            land_all()
-
-    steps(args.warmup)
+        r.render()  # steps are queued back to back (sync only around the timed region)
+        if comm is not None:
+            mg.Comm.gather_bands([comm], [r.out], r.W, r.H, root=0)
+            if args.gather_sync:
+                r.finish()
 
     def sync_all():
         r.finish()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if comm is not None:
+            mg.Comm.barrier([comm])
 
+    for _ in range(args.warmup):
+        step()
     r.k.set_timing(True)
     r.k.reset_stats()
     sync_all()
     t0 = time.perf_counter()
-    steps(args.steps)
+    for _ in range(args.steps):
+        step()
     sync_all()
     elapsed = time.perf_counter() - t0
     ks = r.k.stats()
     r.k.set_timing(False)
-    if dist is not None:
-        import torch
-        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    if comm is not None:
+        elapsed = float(mg.Comm.allreduce([comm], [elapsed], N.COMM_MAX)[0][0])
+
+    check = None
+    if args.check_gather and comm is not None and rank == 0:
+        # the gathered image (every rank's bands, through RCCL) against an unsharded render
+        a = np.empty((r.H * r.W, 4), np.float32)
+        r.ctx.ReadBuffer(r.out, a, blocking=True)
+        ref_out = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16)
+        kf = make_kernel(r.ctx, r.bufs, ref_out, args)
+        r.render(kf)
+        b = np.empty_like(a)
+        r.ctx.ReadBuffer(ref_out, b, blocking=True)
+        same = a.view(np.uint32)[:, :3] == b.view(np.uint32)[:, :3]
+        if not same.all():
+            raise SystemExit(f"check-gather: {int((~same).any(axis=1).sum())} pixels of the gathered image differ")
+        check = f"gathered {r.W}x{r.H} image byte-identical to an unsharded render ({world} ranks)"
+        print(f"check-gather: {check}", file=sys.stderr)
+        kf.release()
+        ref_out.release()
+    if comm is not None:
+        mg.Comm.barrier([comm])
 
     rays_per_step, visits, tests, hits = counts
     ms_step = elapsed * 1e3 / args.steps
     value = rays_per_step * args.steps / elapsed / 1e6
-    # roofline of KernelEntry on rank 0: algorithmic bytes of one launch (one frame of this
-    # rank's tile) / its mean duration
     launches = max(1, ks["launches"])
     kernel_ms = ks["kernel_ms"] / launches
-    accum_ms = ks["accum_ms"] / launches
     frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
-    # fused launches accumulate on a second stream that overlaps the next render (rt_capi.cpp,
-    # RT_ACCUM_OVERLAP): its event span then includes the wait for the render, so it is not a
-    # kernel duration -- the rocprofv3 kernel trace under profiles/ carries that
-    accum_overlapped = frames_per_launch > 1 and os.environ.get("RT_ACCUM_OVERLAP", "1") != "0"
-    local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
-    tile_px = r.pixels
-    alg_bytes = ((48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames
-                 + 32 * tile_px) * frames_per_launch
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-    traffic = None
-    valu = None
-    tpath = os.path.join(REPO, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            key = (f"{args.scene}_{args.width}x{args.height}_f{args.frames}_b{args.bounces}_{args.math}_n{world}"
-                   + ("_fused" if frames_per_launch > 1 else ""))
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
-                insts = tj[key].get("valu_insts_per_launch")
-                if insts and kernel_ms > 0:
-                    # VALU issue: one wave64 VALU instruction holds a SIMD-32 for 2 cycles; 4 SIMDs
-                    # per CU at the 2.4 GHz clock (MI355X_MICROARCH.md).  The binding resource of
-                    # this LDS-resident traversal, next to the HBM roofline the contract asks for.
-                    cap = SIMDS * 2.4e9 * kernel_ms * 1e-3 / 2.0
-                    valu = {"insts_per_launch": int(insts), "issue_frac": round(insts / cap, 4),
-                            "peak_insts_per_s": SIMDS * 2.4e9 / 2.0}
-        except (ValueError, KeyError):
-            traffic = None
-
-    if args.check_gather and final is not None:
-        # rank 0's own bands must have travelled out through RCCL and back into the final image
-        a = np.empty((r.H * r.W, 4), np.float32)
-        b = np.empty_like(a)
-        r.ctx.ReadBuffer(r.out, a)
-        torch.cuda.synchronize()
-        b[:] = final.cpu().numpy().reshape(b.shape)  # the pipelined flow's final image (a tensor)
-        rows = np.concatenate([np.arange(bb * mg.BAND_ROWS, min(r.H, (bb + 1) * mg.BAND_ROWS)) for bb in r.bands])
-        a, b = a.reshape(r.H, r.W, 4)[rows], b.reshape(r.H, r.W, 4)[rows]
-        if not (a.view(np.uint32) == b.view(np.uint32)).all():
-            raise SystemExit("gathered image differs from the rendered bands")
-        print(f"check-gather: {rows.size} rows identical", file=sys.stderr)
+    rl = roofline(args, world, frames_per_launch, kernel_ms, local_counts, r.pixels)
+    rl["accum_overlapped"] = frames_per_launch > 1 and not args.no_accum_overlap
+    if not rl["accum_overlapped"] and frames_per_launch > 1:
+        rl["accum_ms_per_launch"] = round(ks["accum_ms"] / launches, 4)
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        comm.destroy()
         return
     scene_name = "Cornell box" if args.scene == "cornell" else "bunny-class proxy, 69,692 triangles"
     line = {
@@ -393,23 +366,22 @@ def main():
                  "generated bunny-class proxy OBJ (clrt/proxy.py)") + "; rays generated in-kernel",
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
-                   "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh, "parallelism": f"interleaved 8-row bands x{world}" + (
-                       (" + gloo gather to rank 0 (host-staged)" if args.dist_backend == "gloo" else
-                        " + RCCL gather to rank 0" + ("" if args.no_overlap else ", pipelined with the next step"))
-                       if dist is not None else ""),
-                   "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
-                     "frames_per_launch": frames_per_launch, "accum_ms_per_launch": None if accum_overlapped else round(accum_ms, 4),
-                     "accum_overlapped": accum_overlapped,
-                     "alg_bytes_per_launch": int(alg_bytes), "valu": valu},
+                   "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh,
+                   "parallelism": f"interleaved 8-row bands x{world}" + (
+                       " + RCCL gather to rank 0 (librt_hip rtCommEnqueueGatherBands"
+                       + (", host-synchronised)" if args.gather_sync else ", pipelined with the next step)")
+                       if comm is not None else ""),
+                   "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames,
+                   "tuning": args.tune or None},
+        "roofline": rl,
     }
+    if check:
+        line["check_gather"] = check
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(scene, args)
+        line["cpu_baseline"] = cpu_baseline(scene, args, pinned_rays(r, args))
     print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.destroy()
 
 
 if __name__ == "__main__":

@@ -97,7 +97,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size);
  * The accumulation launch runs on a second stream of the context, overlapping the next
  * fused render; every other call on the context (buffer reads/writes/copies, per-frame
  * launches, rtFinish, rtContextGetStream) is ordered after it, so the context still behaves
- * as one in-order queue.  RT_ACCUM_OVERLAP=0 in the environment keeps it on the main stream. */
+ * as one in-order queue.  rtContextSetAccumOverlap(ctx, 0) keeps it on the main stream. */
 int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames);
 
 /* CLContext::ReadBuffer (CLutils.cpp:37-42, non-blocking in the reference) and
@@ -218,6 +218,107 @@ int rtContextGetStream(rt_context ctx, void** hip_stream);
 int rtContextSetReadbackOnAccumStream(rt_context ctx, int enable);
 int rtContextGetAccumStream(rt_context ctx, void** hip_stream);
 int rtContextGetDevice(rt_context ctx, int* device_index);
+
+/* Host-only check (no GPU) of a flattened BVH against the contract KernelEntry relies on
+ * (CLBVHnode.cpp:161-183): interior node i has children i+1 and offset > i+1, both < n_nodes,
+ * axis <= 2; leaves [offset, offset + nPrimitives) lie within the n_tris triangles; every node
+ * but the root has exactly one parent (one tree, every node reachable).  Every launch runs it
+ * on the bound arrays first (RT_INVALID_MEM_OBJECT, never a GPU walk).  *depth = the deepest
+ * leaf's depth. */
+int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
+
+/* Scheduling parameters of the persistent schedules (extension; no effect on results, only on
+ * speed -- every value renders the same bits).  Defaults were swept on MI355X
+ * (profiles/r01/ *_sweep*.txt); these calls exist for re-tuning, replacing environment reads so
+ * that library behaviour does not depend on the caller's environment.  Out-of-range values ->
+ * RT_INVALID_VALUE.
+ *   REFILL_MIN / SHADE_MIN            step schedule, LDS scenes: finish + refill when this many
+ *                                     lanes are free (1-64, default 6); shade when this many are
+ *                                     ready (1-64, default 44)
+ *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (8 / 48)
+ *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)
+ *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64 (128 / 64)
+ *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)
+ *   TOP_NODES                         global path: top-of-tree nodes staged in LDS (0-1024, 384)
+ *   POOL_SHADE / PARK_MIN / LOW_WORK  pool schedule thresholds (64 / 16 / 32)
+ *   TILE_MAJOR                        fused work order: -1 auto (default), 0 frame-major, 1 tile-major
+ *   PERFRAME_SKY                      per-frame sky shortcut: 0 off, 1 large launches (default),
+ *                                     2 always */
+enum rt_tuning {
+    RT_TUNE_REFILL_MIN = 0,
+    RT_TUNE_SHADE_MIN = 1,
+    RT_TUNE_REFILL_MIN_GLOBAL = 2,
+    RT_TUNE_SHADE_MIN_GLOBAL = 3,
+    RT_TUNE_STEP_WEIGHT_NODE = 4,
+    RT_TUNE_STEP_WEIGHT_LEAF = 5,
+    RT_TUNE_CHUNK_PIXELS = 6,
+    RT_TUNE_TAIL_CHUNK = 7,
+    RT_TUNE_BULK_PERCENT = 8,
+    RT_TUNE_TOP_NODES = 9,
+    RT_TUNE_POOL_SHADE = 10,
+    RT_TUNE_PARK_MIN = 11,
+    RT_TUNE_LOW_WORK = 12,
+    RT_TUNE_TILE_MAJOR = 13,
+    RT_TUNE_PERFRAME_SKY = 14
+};
+int rtKernelSetTuning(rt_kernel k, int param, int value);
+int rtKernelGetTuning(rt_kernel k, int param, int* value);
+
+/* Fused frames' accumulation on the context's second stream, overlapping the next render
+ * (default 1), or on the main stream (0).  Synchronises the context. */
+int rtContextSetAccumOverlap(rt_context ctx, int enable);
+
+/* ---- multi-GPU: band sharding + RCCL gather (extension) -----------------------
+ * The reference renders on one OpenCL device (CLRaytracer.cpp:104-120, CLutils.cpp:29).  Pixels
+ * are independent -- the seed depends only on the global work-item id and frameCount
+ * (kernel_bvh.cl:445) and the accumulation is per pixel (:449-455) -- so a frame shards by
+ * interleaved 8-row bands (band b -> rank b % nranks; rtCommShardKernel) rendered at their
+ * global positions, with one exchange at the end: the bands are gathered to a root rank over
+ * RCCL (xGMI), byte-identical to a one-GPU render.
+ *
+ * Communicators: one rank per GPU, either one process per GPU (rtCommGetUniqueId on one rank,
+ * the 128-byte id passed to the others by any host means, rtCommInitRank everywhere) or one
+ * process driving several GPUs, one context each (rtCommInitAll = ncclCommInitAll). */
+typedef struct rt_comm_s* rt_comm;
+#define RT_COMM_ID_BYTES 128
+int rtCommGetUniqueId(void* id /* RT_COMM_ID_BYTES */);
+int rtCommInitRank(rt_context ctx, int nranks, const void* id, int rank, rt_comm* out);
+int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
+int rtCommDestroy(rt_comm comm);
+int rtCommGetRank(rt_comm comm, int* rank, int* nranks);
+/* The kernel renders this rank's bands: rtKernelSetRowInterleave(k, nranks, rank). */
+int rtCommShardKernel(rt_comm comm, rt_kernel k);
+/* Gather the band-sharded image: every rank's bands of its `out` buffer (width x height pixels
+ * of 16 bytes, rendered after rtCommShardKernel) are assembled in the root's `root_dst` (NULL =
+ * the root's own `out`).  `comms`/`outs`: the n_local communicators this host thread drives
+ * (1 per process in the one-process-per-GPU setup) and their output buffers.  Asynchronous and
+ * pipelined: each rank packs its bands after the fused-frame accumulations enqueued so far (on
+ * the context's accumulation stream), RCCL moves them (grouped send/recv: the root receives on
+ * all links at once; its own bands go through RCCL too, a device-local send to itself, so a
+ * world of one runs the same flow) on the communicator's stream and the root unpacks them on a
+ * third stream,
+ * so the next fused render is not held up; two staging slots, so step k's gather overlaps step
+ * k+1's render.  Every later call on a context that reads or writes memory (rtFinish,
+ * rtEnqueueReadBuffer, per-frame launches, ...) is ordered after the gather. */
+int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_local, unsigned width,
+                             unsigned height, int root, rt_mem root_dst);
+/* Blocking reductions of `count` doubles per local rank (values: n_local x count, in place),
+ * op RT_COMM_SUM or RT_COMM_MAX; rtCommBarrier = a one-value reduction. */
+#define RT_COMM_SUM 0
+#define RT_COMM_MAX 1
+int rtCommAllReduceF64(const rt_comm* comms, int n_local, double* values, int count, int op);
+int rtCommBarrier(const rt_comm* comms, int n_local);
+
+/* The pack plan behind the gather (host-only, no GPU needed): the 2-D copies moving rank
+ * `phase`'s bands (period ranks) of a width x height image between the image
+ * ([img_offset + i*img_pitch, +width) bytes) and a dense staging buffer
+ * ([stage_offset + i*width, +width)); at most 2 rects; *staging_bytes = the per-rank staging
+ * size (the largest rank's share). */
+typedef struct rt_rect {
+    uint64_t img_offset, img_pitch, width, rows, stage_offset;
+} rt_rect;
+int rtBandPackPlan(unsigned width, unsigned height, unsigned period, unsigned phase, rt_rect* rects,
+                   int capacity, int* n_rects, size_t* staging_bytes);
 
 /* Library identification (for smoke checks): returns a static string. */
 const char* rtGetBuildInfo(void);

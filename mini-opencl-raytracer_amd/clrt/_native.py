@@ -71,6 +71,11 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB, MATH_SHIPPED = 0, 1, 2
 SCHED_TILES, SCHED_REGEN, SCHED_STEP, SCHED_POOL = 0, 1, 2, 3
+# rt_tuning (rt_hip.h): scheduling parameters, results unchanged
+TUNING = {"refill_min": 0, "shade_min": 1, "refill_min_global": 2, "shade_min_global": 3,
+          "step_weight_node": 4, "step_weight_leaf": 5, "chunk_pixels": 6, "tail_chunk": 7,
+          "bulk_percent": 8, "top_nodes": 9, "pool_shade": 10, "park_min": 11, "low_work": 12,
+          "tile_major": 13, "perframe_sky": 14}
 
 
 class Stats(ctypes.Structure):
@@ -81,6 +86,15 @@ class Stats(ctypes.Structure):
                 ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64),
                 ("sched", ctypes.c_uint64 * 12), ("accum_ms", ctypes.c_double)]
 
+
+class Rect(ctypes.Structure):
+    """rt_rect (rt_hip.h): one 2-D copy of the band gather's pack plan."""
+    _fields_ = [("img_offset", ctypes.c_uint64), ("img_pitch", ctypes.c_uint64), ("width", ctypes.c_uint64),
+                ("rows", ctypes.c_uint64), ("stage_offset", ctypes.c_uint64)]
+
+
+COMM_ID_BYTES = 128
+COMM_SUM, COMM_MAX = 0, 1
 
 _vp = ctypes.c_void_p
 _HIP_PROTOS = {
@@ -119,6 +133,23 @@ _HIP_PROTOS = {
     "rtContextSetReadbackOnAccumStream": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtContextGetAccumStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "rtContextGetDevice": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "rtValidateBVH": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]),
+    "rtKernelSetTuning": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    "rtKernelGetTuning": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "rtContextSetAccumOverlap": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtCommGetUniqueId": (ctypes.c_int, [_vp]),
+    "rtCommInitRank": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rtCommInitAll": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rtCommDestroy": (ctypes.c_int, [_vp]),
+    "rtCommGetRank": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "rtCommShardKernel": (ctypes.c_int, [_vp, _vp]),
+    "rtCommEnqueueGatherBands": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_uint,
+                                                ctypes.c_uint, ctypes.c_int, _vp]),
+    "rtCommAllReduceF64": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.c_int, ctypes.c_int]),
+    "rtCommBarrier": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int]),
+    "rtBandPackPlan": (ctypes.c_int, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(Rect),
+                                      ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)]),
     "rtGetBuildInfo": (ctypes.c_char_p, []),
 }
 HIP_EXPORTS = tuple(_HIP_PROTOS)
@@ -156,6 +187,14 @@ def _load(path: str, protos: dict) -> ctypes.CDLL:
         fn.argtypes = args
     _libs[path] = lib
     return lib
+
+
+def validate_bvh(nodes: np.ndarray, n_tris: int) -> int:
+    """rtValidateBVH (host-only): the BVH depth, or RTError(CL_INVALID_MEM_OBJECT)."""
+    nodes = np.ascontiguousarray(nodes)
+    d = ctypes.c_int()
+    check(hip_lib().rtValidateBVH(nodes.ctypes.data, len(nodes), int(n_tris), ctypes.byref(d)), "Invalid BVH")
+    return d.value
 
 
 def hip_lib() -> ctypes.CDLL:

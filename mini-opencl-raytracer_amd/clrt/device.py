@@ -92,6 +92,10 @@ class CLContext:
         check(self._lib.rtContextGetAccumStream(self.handle, ctypes.byref(s)), "accumulation stream")
         return int(s.value or 0)
 
+    def set_accum_overlap(self, enable: bool) -> None:
+        """rtContextSetAccumOverlap: fused frames' accumulation beside the next render (default)."""
+        check(self._lib.rtContextSetAccumOverlap(self.handle, int(bool(enable))), "accumulation overlap")
+
     def set_readback_on_accum_stream(self, enable: bool) -> None:
         check(self._lib.rtContextSetReadbackOnAccumStream(self.handle, int(bool(enable))), "readback stream")
 
@@ -174,6 +178,15 @@ class CLKernel:
 
     def set_schedule(self, sched: int) -> None:
         check(self._lib.rtKernelSetSchedule(self.handle, int(sched)), "schedule")
+
+    def set_tuning(self, name: str, value: int) -> None:
+        """rtKernelSetTuning: a scheduling parameter by name (N.TUNING); results are unchanged."""
+        check(self._lib.rtKernelSetTuning(self.handle, N.TUNING[name], int(value)), f"tuning {name}")
+
+    def get_tuning(self, name: str) -> int:
+        v = ctypes.c_int()
+        check(self._lib.rtKernelGetTuning(self.handle, N.TUNING[name], ctypes.byref(v)), f"tuning {name}")
+        return int(v.value)
 
     def set_row_interleave(self, period: int, phase: int) -> None:
         check(self._lib.rtKernelSetRowInterleave(self.handle, int(period), int(phase)), "row interleave")

@@ -11,14 +11,24 @@ output buffer at their global positions; to assemble the image the bands are pac
 xGMI on the GPU box: grouped send/recv, so the root receives on all its links at once), and
 unpacked on the root with the inverse 2-D copy.
 
-The plans below are pure index math, shared by the device path (clrt.CLContext 2-D copies)
-and the numpy path the CPU tests use.
+The product path is the library's RCCL communicator (``Comm`` below over rtComm* in
+include/rt_hip.h, csrc/rt_comm.cpp): pack on the context's accumulation stream, grouped
+send/recv to the root on the communicator's stream, unpack on a third stream -- no torch
+and no second HIP runtime in the process.  The plans below are pure index math, the same
+as the library's rtBandPackPlan (tests compare them), and drive the numpy path the CPU tests
+use over torch.distributed/gloo.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
+
+from . import _native as N
+from ._native import check
 
 BAND_ROWS = 8          # = the 8x8 tile height of the regen/step schedules
 PIXEL_BYTES = 16       # one float3 slot of the output buffer
@@ -102,3 +112,116 @@ def gather_to_root(dist, tensor, rank: int, world: int):
     out = [torch.empty_like(tensor) for _ in range(world)] if rank == 0 else None
     dist.gather(tensor, out, dst=0)
     return out
+
+
+def native_pack_plan(width: int, height: int, period: int, phase: int) -> tuple[list[Rect], int]:
+    """rtBandPackPlan: the library's plan (host-only, loads librt_hip.so without a GPU)."""
+    lib = N.hip_lib()
+    rects = (N.Rect * 2)()
+    n = ctypes.c_int()
+    sb = ctypes.c_size_t()
+    check(lib.rtBandPackPlan(width, height, period, phase, rects, 2, ctypes.byref(n), ctypes.byref(sb)), "band plan")
+    return [Rect(r.img_offset, r.img_pitch, r.width, r.rows, r.stage_offset) for r in rects[:n.value]], sb.value
+
+
+class Comm:
+    """One rank's RCCL communicator (rt_comm): band sharding + the pipelined band gather."""
+
+    def __init__(self, handle: int, ctx):
+        self._lib = N.hip_lib()
+        self.handle = handle
+        self.ctx = ctx
+        r, n = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.rtCommGetRank(handle, ctypes.byref(r), ctypes.byref(n)), "comm rank")
+        self.rank, self.nranks = r.value, n.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(N.COMM_ID_BYTES)
+        check(N.hip_lib().rtCommGetUniqueId(buf), "comm unique id")
+        return buf.raw
+
+    @classmethod
+    def init_rank(cls, ctx, nranks: int, uid: bytes, rank: int) -> "Comm":
+        """One process per GPU (ncclCommInitRank)."""
+        assert len(uid) == N.COMM_ID_BYTES
+        h = ctypes.c_void_p()
+        check(N.hip_lib().rtCommInitRank(ctx.handle, nranks, uid, rank, ctypes.byref(h)), "comm init rank")
+        return cls(h.value, ctx)
+
+    @classmethod
+    def init_all(cls, ctxs) -> list["Comm"]:
+        """One process driving len(ctxs) GPUs (ncclCommInitAll)."""
+        n = len(ctxs)
+        hs = (ctypes.c_void_p * n)(*[c.handle for c in ctxs])
+        out = (ctypes.c_void_p * n)()
+        check(N.hip_lib().rtCommInitAll(hs, n, out), "comm init all")
+        return [cls(out[i], ctxs[i]) for i in range(n)]
+
+    def shard(self, kernel) -> None:
+        """The kernel renders this rank's interleaved bands (rtCommShardKernel)."""
+        check(self._lib.rtCommShardKernel(self.handle, kernel.handle), "shard kernel")
+
+    @staticmethod
+    def gather_bands(comms, outs, width: int, height: int, root: int = 0, dst=None) -> None:
+        """rtCommEnqueueGatherBands over the communicators this thread drives."""
+        n = len(comms)
+        hc = (ctypes.c_void_p * n)(*[c.handle for c in comms])
+        ho = (ctypes.c_void_p * n)(*[o.handle for o in outs])
+        check(comms[0]._lib.rtCommEnqueueGatherBands(hc, ho, n, width, height, root, dst.handle if dst else None),
+              "gather bands")
+
+    @staticmethod
+    def allreduce(comms, values, op: int = N.COMM_SUM) -> np.ndarray:
+        """Blocking reduction of float64 values (n_local x count)."""
+        v = np.ascontiguousarray(np.asarray(values, np.float64).reshape(len(comms), -1))
+        hc = (ctypes.c_void_p * len(comms))(*[c.handle for c in comms])
+        check(comms[0]._lib.rtCommAllReduceF64(hc, len(comms), v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                               v.shape[1], op), "allreduce")
+        return v
+
+    @staticmethod
+    def barrier(comms) -> None:
+        hc = (ctypes.c_void_p * len(comms))(*[c.handle for c in comms])
+        check(comms[0]._lib.rtCommBarrier(hc, len(comms)), "barrier")
+
+    def destroy(self) -> None:
+        if self.handle:
+            self._lib.rtCommDestroy(self.handle)
+            self.handle = None
+
+
+def file_rendezvous(rank: int, world: int, make_id, timeout: float = 300.0) -> bytes:
+    """Hand rank 0's communicator id to the other ranks of ONE node through a file (no torch,
+    no sockets): the path is keyed by the launcher's pid (every rank of a torch.distributed.run
+    job has the same parent) and MASTER_PORT; RT_COMM_ID_FILE overrides it."""
+    path = os.environ.get("RT_COMM_ID_FILE") or os.path.join(
+        "/tmp", f"rt_comm_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.id")
+    if rank == 0:
+        uid = make_id()
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return uid
+    t0 = time.monotonic()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                uid = f.read()
+            if len(uid) == N.COMM_ID_BYTES:
+                return uid
+        except FileNotFoundError:
+            pass
+        if time.monotonic() - t0 > timeout:
+            raise TimeoutError(f"rank {rank}: no communicator id at {path} after {timeout:.0f} s")
+        time.sleep(0.05)
+
+
+def rendezvous_cleanup() -> None:
+    path = os.environ.get("RT_COMM_ID_FILE") or os.path.join(
+        "/tmp", f"rt_comm_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.id")
+    try:
+        os.unlink(path)
+    except FileNotFoundError:
+        pass

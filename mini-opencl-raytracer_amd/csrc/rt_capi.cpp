@@ -24,6 +24,7 @@
 #include "../../include/rt_cl_types.h"
 #include "../../include/rt_hip.h"
 #include "rt_bvh.hpp"
+#include "rt_internal.hpp"
 #include "rt_kernels.hpp"
 
 namespace {
@@ -33,56 +34,10 @@ constexpr uint64_t kKnownFlags =
 constexpr int kStatWords = 20;                // rt_stats counters kept on the device
 constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
 
-int map_hip(hipError_t e) {
-    switch (e) {
-        case hipSuccess: return RT_SUCCESS;
-        case hipErrorOutOfMemory: return RT_MEM_OBJECT_ALLOCATION_FAILURE;
-        case hipErrorNoDevice:
-        case hipErrorInvalidDevice: return RT_DEVICE_NOT_FOUND;
-        case hipErrorLaunchOutOfResources: return RT_OUT_OF_RESOURCES;
-        default: return RT_INVALID_OPERATION;
-    }
-}
-
 }  // namespace
 
-struct rt_context_s {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int num_cus = 0;
-    // Fused frames: the accumulation launch runs on its own stream, so it overlaps the next
-    // render (its waves fit beside the render grid: RT_ACCUM_VGPRS).  Every other operation
-    // goes through qs(), which first makes the context's in-order stream wait for the
-    // accumulations enqueued so far -- to the caller the context stays one in-order queue.
-    hipStream_t astream = nullptr;
-    hipEvent_t atail = nullptr;  // last accumulation enqueued on astream
-    bool apending = false;
-    bool overlap = true;  // RT_ACCUM_OVERLAP=0: accumulate on the main stream
-    // rtContextSetReadbackOnAccumStream: buffer -> pointer rect copies go to astream, right after
-    // the accumulation they read, so the main stream runs on into the next render
-    bool readback_on_astream = false;
-};
-
-namespace {
-// The context's stream, after every pending accumulation (see rt_context_s).
-hipStream_t qs(rt_context ctx) {
-    if (ctx->apending) {
-        (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
-        ctx->apending = false;
-    }
-    return ctx->stream;
-}
-}  // namespace
-
-struct rt_mem_s {
-    rt_context ctx = nullptr;
-    void* dptr = nullptr;
-    size_t size = 0;
-    uint64_t flags = 0;
-    std::vector<uint8_t> shadow;  // host copy of the bytes (valid when shadow_valid)
-    bool shadow_valid = false;
-    uint64_t generation = 0;      // bumped on every host write
-};
+using rti::map_hip;
+using rti::qs;
 
 struct rt_kernel_s {
     rt_context ctx = nullptr;
@@ -105,8 +60,8 @@ struct rt_kernel_s {
     uint32_t* work_counter = nullptr;  // regen schedule chunk counter
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
-    int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major (RT_TILE_MAJOR)
-    int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always (RT_PF_SKY)
+    int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
+    int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
@@ -166,16 +121,22 @@ int host_bytes(rt_mem m, std::vector<uint8_t>& tmp, const uint8_t** out) {
     return RT_SUCCESS;
 }
 
-// Validate the flattened BVH (CLBVHnode.cpp:161-183 contract) and return its depth.
+// Validate the flattened BVH (CLBVHnode.cpp:161-183 contract) and return its depth.  Every
+// node is checked, reachable or not (the skip/record builders below walk all of them), and
+// the array must be exactly one tree: each node but the root has exactly one parent.  Since a
+// parent's index is smaller than its children's, that makes every node reachable from node 0
+// and the skip-pointer walk a finite depth-first order (a child shared by two parents would
+// make it loop).
 int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* depth_out) {
     if (n == 0) return RT_INVALID_MEM_OBJECT;
     std::vector<int> depth(n, -1);
+    std::vector<uint8_t> parents(n, 0);
     depth[0] = 0;
     int max_depth = 0;
     // children have larger indices than their parent, so one forward sweep sets depths
     for (uint32_t i = 0; i < n; ++i) {
-        if (depth[i] < 0) continue;  // unreachable node: never visited by the kernel
         const rt_cl_bvh_node& x = nd[i];
+        if (i > 0 && parents[i] != 1) return RT_INVALID_MEM_OBJECT;  // orphan: unreachable
         if (x.nPrimitives > 0) {
             if ((uint64_t)x.offset + x.nPrimitives > n_tris) return RT_INVALID_MEM_OBJECT;
             max_depth = std::max(max_depth, depth[i]);
@@ -183,8 +144,9 @@ int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* dept
             if (x.axis > 2) return RT_INVALID_MEM_OBJECT;
             const uint64_t a = (uint64_t)i + 1, b = x.offset;
             if (a >= n || b >= n || b <= a) return RT_INVALID_MEM_OBJECT;
-            depth[a] = std::max(depth[a], depth[i] + 1);
-            depth[b] = std::max(depth[b], depth[i] + 1);
+            if (parents[a]++ != 0 || parents[b]++ != 0) return RT_INVALID_MEM_OBJECT;  // shared child
+            depth[a] = depth[i] + 1;
+            depth[b] = depth[i] + 1;
         }
     }
     *depth_out = max_depth;
@@ -467,13 +429,14 @@ int rtCreateContext(int device_index, rt_context* out) {
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->astream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->atail, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->mtail, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->gtail, hipEventDisableTiming);
     if (e != hipSuccess) {
         if (c->stream) (void)hipStreamDestroy(c->stream);
         if (c->astream) (void)hipStreamDestroy(c->astream);
         delete c;
         return RT_INVALID_COMMAND_QUEUE;
     }
-    if (const char* v = std::getenv("RT_ACCUM_OVERLAP")) c->overlap = std::atoi(v) != 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device_index) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     if (c->num_cus <= 0) c->num_cus = 256;
@@ -489,6 +452,8 @@ int rtReleaseContext(rt_context ctx) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->astream);
     (void)hipEventDestroy(ctx->atail);
+    (void)hipEventDestroy(ctx->mtail);
+    (void)hipEventDestroy(ctx->gtail);
     delete ctx;
     return RT_SUCCESS;
 }
@@ -555,27 +520,6 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     rt_kernel k = new (std::nothrow) rt_kernel_s();
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
-    if (const char* v = std::getenv("RT_REFILL_MIN"))
-        k->refill_min = k->refill_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_SHADE_MIN"))
-        k->shade_min = k->shade_min_g = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_TILE_MAJOR")) k->tile_major = std::max(-1, std::min(1, std::atoi(v)));
-    if (const char* v = std::getenv("RT_PF_SKY")) k->pf_sky = std::max(0, std::min(2, std::atoi(v)));
-    if (const char* v = std::getenv("RT_W_NODE")) k->w_node = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
-    if (const char* v = std::getenv("RT_W_LEAF")) k->w_leaf = (uint32_t)std::max(1, std::min(1000, std::atoi(v)));
-    if (const char* v = std::getenv("RT_CHUNK"))
-        k->chunk_pixels = (uint32_t)std::max(1, std::min(64, std::atoi(v) / 64)) * 64u;
-    if (const char* v = std::getenv("RT_TAIL_CHUNK"))
-        k->tail_chunk = (uint32_t)std::max(1, std::min(64, std::atoi(v) / 64)) * 64u;
-    if (const char* v = std::getenv("RT_BULK_PERCENT")) k->bulk_percent = (uint32_t)std::max(0, std::min(100, std::atoi(v)));
-    if (const char* v = std::getenv("RT_TOP_NODES")) k->top_limit = (uint32_t)std::max(0, std::min(1024, std::atoi(v)));
-    if (const char* v = std::getenv("RT_POOL_SHADE")) k->pool_shade = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_PARK_MIN")) k->park_min = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_LOW_WORK")) k->low_work = (uint32_t)std::max(1, std::min(128, std::atoi(v)));
-    if (const char* v = std::getenv("RT_SCHED")) {
-        const int sv = std::atoi(v);
-        if (sv >= 0 && sv < rtk::kNumSched) k->sched = sv;
-    }
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
@@ -995,10 +939,16 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
     if (src_offset + (rows - 1) * src_pitch + width_bytes > src->size) return RT_INVALID_VALUE;
     if (ctx->readback_on_astream && ctx->overlap) {
-        // after every accumulation enqueued so far, before any later one (astream is in order);
-        // later main-stream work that joins (qs) waits for the copy too
-        hipError_t e = hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
-                                        width_bytes, rows, hipMemcpyDeviceToDevice, ctx->astream);
+        // after every accumulation enqueued so far, before any later one (astream is in order),
+        // and after everything already queued on the main stream (a per-frame launch writes
+        // `out` there; a fused render's tail is the accumulation's own dependency, so waiting on
+        // it costs the overlap nothing); later main-stream work that joins (qs) waits for the
+        // copy too
+        hipError_t e = hipEventRecord(ctx->mtail, ctx->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->astream, ctx->mtail, 0);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
+                                 width_bytes, rows, hipMemcpyDeviceToDevice, ctx->astream);
         if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
         if (e == hipSuccess) ctx->apending = true;
         return map_hip(e);
@@ -1134,6 +1084,79 @@ int rtContextGetStream(rt_context ctx, void** s) {
 int rtContextGetDevice(rt_context ctx, int* d) {
     if (!ctx || !d) return RT_INVALID_VALUE;
     *d = ctx->device;
+    return RT_SUCCESS;
+}
+
+int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth) {
+    if (!nodes || n_nodes == 0 || n_nodes >= (1u << 30) || n_tris >= (1ull << 32)) return RT_INVALID_VALUE;
+    int d = 0;
+    int rc = check_nodes(static_cast<const rt_cl_bvh_node*>(nodes), (uint32_t)n_nodes, (uint32_t)n_tris, &d);
+    if (rc == RT_SUCCESS && depth) *depth = d;
+    return rc;
+}
+
+int rtKernelSetTuning(rt_kernel k, int param, int value) {
+    if (!k) return RT_INVALID_KERNEL;
+    auto in = [&](int lo, int hi) { return value >= lo && value <= hi; };
+    switch (param) {
+        case RT_TUNE_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min = (uint32_t)value; break;
+        case RT_TUNE_SHADE_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->shade_min = (uint32_t)value; break;
+        case RT_TUNE_REFILL_MIN_GLOBAL: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min_g = (uint32_t)value; break;
+        case RT_TUNE_SHADE_MIN_GLOBAL: if (!in(1, 64)) return RT_INVALID_VALUE; k->shade_min_g = (uint32_t)value; break;
+        case RT_TUNE_STEP_WEIGHT_NODE: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_node = (uint32_t)value; break;
+        case RT_TUNE_STEP_WEIGHT_LEAF: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_leaf = (uint32_t)value; break;
+        case RT_TUNE_CHUNK_PIXELS:
+            if (!in(64, 4096) || value % 64) return RT_INVALID_VALUE;
+            k->chunk_pixels = (uint32_t)value;
+            break;
+        case RT_TUNE_TAIL_CHUNK:
+            if (!in(64, 4096) || value % 64) return RT_INVALID_VALUE;
+            k->tail_chunk = (uint32_t)value;
+            break;
+        case RT_TUNE_BULK_PERCENT: if (!in(0, 100)) return RT_INVALID_VALUE; k->bulk_percent = (uint32_t)value; break;
+        case RT_TUNE_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->top_limit = (uint32_t)value; k->packed_nodes_gen = ~0ull; break;
+        case RT_TUNE_POOL_SHADE: if (!in(1, 64)) return RT_INVALID_VALUE; k->pool_shade = (uint32_t)value; break;
+        case RT_TUNE_PARK_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->park_min = (uint32_t)value; break;
+        case RT_TUNE_LOW_WORK: if (!in(1, 128)) return RT_INVALID_VALUE; k->low_work = (uint32_t)value; break;
+        case RT_TUNE_TILE_MAJOR: if (!in(-1, 1)) return RT_INVALID_VALUE; k->tile_major = value; break;
+        case RT_TUNE_PERFRAME_SKY: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_sky = value; break;
+        default: return RT_INVALID_VALUE;
+    }
+    return RT_SUCCESS;
+}
+
+int rtKernelGetTuning(rt_kernel k, int param, int* value) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (!value) return RT_INVALID_VALUE;
+    switch (param) {
+        case RT_TUNE_REFILL_MIN: *value = (int)k->refill_min; break;
+        case RT_TUNE_SHADE_MIN: *value = (int)k->shade_min; break;
+        case RT_TUNE_REFILL_MIN_GLOBAL: *value = (int)k->refill_min_g; break;
+        case RT_TUNE_SHADE_MIN_GLOBAL: *value = (int)k->shade_min_g; break;
+        case RT_TUNE_STEP_WEIGHT_NODE: *value = (int)k->w_node; break;
+        case RT_TUNE_STEP_WEIGHT_LEAF: *value = (int)k->w_leaf; break;
+        case RT_TUNE_CHUNK_PIXELS: *value = (int)k->chunk_pixels; break;
+        case RT_TUNE_TAIL_CHUNK: *value = (int)k->tail_chunk; break;
+        case RT_TUNE_BULK_PERCENT: *value = (int)k->bulk_percent; break;
+        case RT_TUNE_TOP_NODES: *value = (int)k->top_limit; break;
+        case RT_TUNE_POOL_SHADE: *value = (int)k->pool_shade; break;
+        case RT_TUNE_PARK_MIN: *value = (int)k->park_min; break;
+        case RT_TUNE_LOW_WORK: *value = (int)k->low_work; break;
+        case RT_TUNE_TILE_MAJOR: *value = k->tile_major; break;
+        case RT_TUNE_PERFRAME_SKY: *value = k->pf_sky; break;
+        default: return RT_INVALID_VALUE;
+    }
+    return RT_SUCCESS;
+}
+
+int rtContextSetAccumOverlap(rt_context ctx, int enable) {
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    // switching modes: everything queued so far completes on the old arrangement first
+    hipError_t e = hipStreamSynchronize(qs(ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->astream);
+    if (e != hipSuccess) return map_hip(e);
+    ctx->overlap = enable != 0;
     return RT_SUCCESS;
 }
 

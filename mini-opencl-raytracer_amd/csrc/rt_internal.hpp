@@ -1,0 +1,71 @@
+// rt_internal.hpp -- objects shared by the C ABI translation units (rt_capi.cpp, rt_comm.cpp):
+// the context (cl::Context + in-order cl::CommandQueue, CLutils.cpp:9-35) and the buffer
+// (cl::Buffer, CLBVHnode.cpp:215-236).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+
+struct rt_context_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 0;
+    // Fused frames: the accumulation launch runs on its own stream, so it overlaps the next
+    // render (its waves fit beside the render grid: RT_ACCUM_VGPRS).  Every other operation
+    // goes through qs(), which first makes the context's in-order stream wait for the
+    // accumulations enqueued so far -- to the caller the context stays one in-order queue.
+    hipStream_t astream = nullptr;
+    hipEvent_t atail = nullptr;  // last accumulation enqueued on astream
+    hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
+    bool apending = false;
+    bool overlap = true;  // rtContextSetAccumOverlap(ctx, 0): accumulate on the main stream
+    // rtContextSetReadbackOnAccumStream: buffer -> pointer rect copies go to astream, right after
+    // the accumulation they read, so the main stream runs on into the next render
+    bool readback_on_astream = false;
+    // multi-GPU gather (rt_comm.cpp) in flight on the communicator's streams: joined by qs() like
+    // the accumulations, so reads of the gathered image are ordered after it
+    hipEvent_t gtail = nullptr;
+    bool gpending = false;
+};
+
+struct rt_mem_s {
+    rt_context ctx = nullptr;
+    void* dptr = nullptr;
+    size_t size = 0;
+    uint64_t flags = 0;
+    std::vector<uint8_t> shadow;  // host copy of the bytes (valid when shadow_valid)
+    bool shadow_valid = false;
+    uint64_t generation = 0;      // bumped on every host write
+};
+
+namespace rti {
+
+inline int map_hip(hipError_t e) {
+    switch (e) {
+        case hipSuccess: return RT_SUCCESS;
+        case hipErrorOutOfMemory: return RT_MEM_OBJECT_ALLOCATION_FAILURE;
+        case hipErrorNoDevice:
+        case hipErrorInvalidDevice: return RT_DEVICE_NOT_FOUND;
+        case hipErrorLaunchOutOfResources: return RT_OUT_OF_RESOURCES;
+        default: return RT_INVALID_OPERATION;
+    }
+}
+
+// The context's stream, after every pending accumulation and gather (see rt_context_s).
+inline hipStream_t qs(rt_context ctx) {
+    if (ctx->apending) {
+        (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
+        ctx->apending = false;
+    }
+    if (ctx->gpending) {
+        (void)hipStreamWaitEvent(ctx->stream, ctx->gtail, 0);
+        ctx->gpending = false;
+    }
+    return ctx->stream;
+}
+
+}  // namespace rti

@@ -7,8 +7,15 @@
 // ++m_FrameCount).  The GL blit is replaced by the image writer (rt_image.h; rows flipped: row 0 of the
 // output is the bottom of the image, as glTexSubImage2D shows it).
 //
-// usage: rt_render [obj=path] [w=W] [h=H] [frames=N] [bounces=B] [light=T] [sky=S]
-//                  [out=file.ppm|file.png] [device=D] [math=shipped|devicelib|pinned]
+// usage: rt_render [scene=path.rtscene | obj=path.obj] [w=W] [h=H] [frames=N] [bounces=B]
+//                  [light=T] [sky=S] [out=file.ppm|file.png] [raw=file.f32] [device=D]
+//                  [math=shipped|devicelib|pinned]
+// The default scene is the Cornell box's binary scene cache next to the build
+// (scenes/generated/cornell.rtscene, written by __graft_entry__.build() from the committed
+// arrays); obj= parses an OBJ/MTL pair instead (CLOBJloader).  raw= also writes the output
+// buffer's float3 slots (16 B per pixel, row 0 first) for bit-level checks.
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -35,10 +42,27 @@ std::string arg(int argc, char** argv, const char* key, const char* dflt) {
     return dflt;
 }
 
+// <repo>/scenes/generated/cornell.rtscene, from this executable's location
+// (<repo>/mini-opencl-raytracer_amd/bin/rt_render)
+std::string default_scene() {
+    char buf[4096];
+    const ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+    if (n <= 0) return "scenes/generated/cornell.rtscene";
+    std::string p(buf, (size_t)n);
+    for (int up = 0; up < 3; ++up) {
+        const size_t k = p.find_last_of('/');
+        if (k == std::string::npos) return "scenes/generated/cornell.rtscene";
+        p.resize(k);
+    }
+    return p + "/scenes/generated/cornell.rtscene";
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
-    const std::string obj = arg(argc, argv, "obj", "scenes/cornell.obj");
+    const std::string obj = arg(argc, argv, "obj", "");
+    const std::string cache = arg(argc, argv, "scene", obj.empty() ? default_scene().c_str() : "");
+    const std::string raw = arg(argc, argv, "raw", "");
     const unsigned W = (unsigned)std::atoi(arg(argc, argv, "w", "1920").c_str());
     const unsigned H = (unsigned)std::atoi(arg(argc, argv, "h", "1080").c_str());
     const int frames = std::atoi(arg(argc, argv, "frames", "8").c_str());
@@ -65,7 +89,10 @@ int main(int argc, char** argv) {
 
         // CLOBJloader::Load + CLBVHScene::CreateBVHTrees (CLEngineBase.cpp:173-179)
         rt_scene* scene = nullptr;
-        rtcl::check(rtsLoadOBJ(obj.c_str(), 4, &scene), "Failed to load scene");
+        if (!cache.empty())
+            rtcl::check(rtsLoadScene(cache.c_str(), &scene), ("Failed to load scene " + cache).c_str());
+        else
+            rtcl::check(rtsLoadOBJ(obj.c_str(), 4, &scene), ("Failed to load scene " + obj).c_str());
         const rt_cl_triangle* tris;
         const rt_cl_bvh_node* nodes;
         const rt_cl_material* mats;
@@ -109,6 +136,15 @@ int main(int argc, char** argv) {
         const bool png = out.size() > 4 && out.compare(out.size() - 4, 4, ".png") == 0;
         const int wrc = png ? rtiWritePNG(out.c_str(), pixels.data(), W, H) : rtiWritePPM(out.c_str(), pixels.data(), W, H);
         if (wrc) std::fprintf(stderr, "writing %s failed: %d\n", out.c_str(), wrc);
+        if (!raw.empty()) {
+            FILE* f = std::fopen(raw.c_str(), "wb");
+            if (!f || std::fwrite(pixels.data(), sizeof(float), pixels.size(), f) != pixels.size()) {
+                std::fprintf(stderr, "writing %s failed\n", raw.c_str());
+                if (f) std::fclose(f);
+                return 1;
+            }
+            std::fclose(f);
+        }
     } catch (const rtcl::CLException& ex) {
         std::fprintf(stderr, "Caught exception: %s\n", ex.what());
         return 1;

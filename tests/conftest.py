@@ -36,16 +36,3 @@ def oracle_mod():
 
 def reference_available() -> bool:
     return os.path.isdir(REFERENCE)
-
-
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first(request):
-    """torch bundles its own HIP runtime next to the one librt_hip.so links; torch's must
-    initialise first in a process (as bench.py does), or it reports no GPUs.  Only on a
-    GPU session (a `-m gpu` selection); a CPU run never touches HIP."""
-    markexpr = request.config.getoption("-m") or ""
-    if "gpu" in markexpr and "not gpu" not in markexpr:
-        import torch
-        if torch.cuda.is_available():
-            torch.zeros(1, device="cuda:0")
-    yield

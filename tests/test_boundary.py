@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 import clrt
@@ -50,8 +51,7 @@ def test_build_info_without_gpu():
 
 def test_no_gpu_fails_loudly():
     """Without a GPU the product raises (no silent CPU fallback)."""
-    import torch
-    if torch.cuda.device_count() > 0:
+    if os.path.exists("/dev/kfd"):
         pytest.skip("GPU present")
     with pytest.raises(clrt.RTError) as e:
         clrt.CLContext(0)
@@ -74,3 +74,68 @@ def test_error_strings_match_cl_names():
     assert clrt.error_string(-52) == "CL_INVALID_KERNEL_ARGS"
     e = clrt.RTError("Failed to enqueue kernel", -63)
     assert str(e) == "Failed to enqueue kernel (CL_INVALID_GLOBAL_WORK_SIZE)"
+
+
+# ---- host-side BVH validation (rtValidateBVH; every launch runs it first) -------------------
+def _leaf(node, first, count):
+    node["nPrimitives"] = count
+    node["offset"] = first
+
+
+def _interior(node, second, axis=0):
+    node["nPrimitives"] = 0
+    node["offset"] = second
+    node["axis"] = axis
+
+
+def test_validate_bvh_accepts_reference_tree(cornell):
+    from clrt import _native as N
+    assert N.validate_bvh(cornell.nodes, len(cornell.triangles)) == 6  # depth 7 levels: 0..6
+
+
+def test_validate_bvh_rejects_shared_child():
+    """0 -> (1, 3), 1 -> (2, 3): node 3 has two parents; the skip-pointer walk would loop."""
+    from clrt import _native as N
+    nd = np.zeros(4, N.NODE_DTYPE)
+    _interior(nd[0], 3)
+    _interior(nd[1], 3)
+    _leaf(nd[2], 0, 1)
+    _leaf(nd[3], 1, 1)
+    with pytest.raises(clrt.RTError) as e:
+        N.validate_bvh(nd, 2)
+    assert e.value.code == -38
+
+
+def test_validate_bvh_rejects_unreachable_interior_with_bad_offset():
+    """An unreachable interior node whose offset is out of range is still rejected (the
+    record builders walk every node)."""
+    from clrt import _native as N
+    nd = np.zeros(4, N.NODE_DTYPE)
+    _interior(nd[0], 2)
+    _leaf(nd[1], 0, 1)
+    _leaf(nd[2], 1, 1)
+    _interior(nd[3], 99)
+    with pytest.raises(clrt.RTError):
+        N.validate_bvh(nd, 2)
+    _leaf(nd[3], 0, 1)  # well-formed but orphaned
+    with pytest.raises(clrt.RTError):
+        N.validate_bvh(nd, 2)
+
+
+@pytest.mark.parametrize("case", ["cycle", "leaf_range", "axis", "backward"])
+def test_validate_bvh_rejects_malformed(cornell, case):
+    from clrt import _native as N
+    bad = cornell.nodes.copy()
+    interior = np.flatnonzero(bad["nPrimitives"] == 0)
+    leaf = np.flatnonzero(bad["nPrimitives"] > 0)[0]
+    if case == "cycle":
+        bad["offset"][interior[0]] = interior[0]
+    elif case == "leaf_range":
+        bad["offset"][leaf] = len(cornell.triangles) - 1
+        bad["nPrimitives"][leaf] = 2
+    elif case == "axis":
+        bad["axis"][interior[1]] = 3
+    else:
+        bad["offset"][interior[2]] = interior[2] - 1
+    with pytest.raises(clrt.RTError):
+        N.validate_bvh(bad, len(cornell.triangles))

@@ -13,8 +13,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _render(scene, W, H, first, n, fused, math=N.MATH_SHIPPED, bounces=9, interleave=None,
-            work_range=None, force_global=False, sched=N.SCHED_STEP, pre=None):
+            work_range=None, force_global=False, sched=N.SCHED_STEP, pre=None, tuning=None):
     r = HipRenderer(scene, W, H, math=math, hits=True, stats=True, force_global=force_global, sched=sched)
+    for name, value in (tuning or {}).items():
+        r.k.set_tuning(name, value)
     kw = dict(light_bounces=bounces, interleave=interleave, work_range=work_range)
     if pre is not None:  # earlier frames already in the buffer
         for f in pre:
@@ -148,12 +150,12 @@ def test_overlapped_accumulation_stays_in_order(cornell):
 
 
 @pytest.mark.parametrize("force_global", [False, True])
-def test_fused_tile_major_order(cornell, monkeypatch, force_global):
-    """Tile-major work order (RT_TILE_MAJOR=1; chosen automatically for large launches on the
+def test_fused_tile_major_order(cornell, force_global):
+    """Tile-major work order (tile_major 1; chosen automatically for large launches on the
     HBM/L2 scene path): the frames of a tile back to back -- same bits as per-frame launches."""
-    monkeypatch.setenv("RT_TILE_MAJOR", "1")
     W, H = 248, 136
-    _same(_render(cornell, W, H, 2, 7, True, force_global=force_global, interleave=(2, 1)),
+    _same(_render(cornell, W, H, 2, 7, True, force_global=force_global, interleave=(2, 1),
+                  tuning={"tile_major": 1}),
           _render(cornell, W, H, 2, 7, False, force_global=force_global, interleave=(2, 1)))
 
 
@@ -161,18 +163,17 @@ def test_readback_on_accum_stream(cornell):
     """rtContextSetReadbackOnAccumStream: a rect copy of the output queued after a fused launch
     runs right after that launch's accumulation on the accumulation stream, so it holds that
     step's image even though the next fused launch is queued before anything waits for it."""
-    import torch
-    torch.zeros(1, device="cuda:0")  # torch's HIP context before the library's
     W, H = 224, 128
     r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
     r.ctx.set_readback_on_accum_stream(True)
-    dst = torch.empty(W * H * 4, dtype=torch.float32, device="cuda:0")
+    dst = r.ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
     r.frame(1, n_frames=8, light_bounces=9)
-    r.ctx.CopyRectToDevicePointer(r.out, 0, W * 16, W * 16, H, dst.data_ptr(), W * 16)
+    r.ctx.CopyRectToDevicePointer(r.out, 0, W * 16, W * 16, H, dst.device_pointer(), W * 16)
     r.frame(9, n_frames=8, light_bounces=9)
-    torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(r.ctx.accum_stream()))
-    step1 = dst.cpu().numpy().reshape(W * H, 4)
+    step1 = np.zeros((W * H, 4), np.float32)
+    r.ctx.ReadBuffer(dst, step1, blocking=True)  # ordered after the copy (rtEnqueueReadBuffer joins)
     step2 = r.result()
+    dst.release()
     r.close()
     ref = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
     ref.frame(1, n_frames=8, light_bounces=9)
@@ -182,3 +183,26 @@ def test_readback_on_accum_stream(cornell):
     ref.close()
     assert step1.tobytes() == want1.tobytes()
     assert step2.tobytes() == want2.tobytes()
+
+
+@pytest.mark.parametrize("frames", [1, 9])
+def test_readback_on_accum_stream_after_per_frame_launches(cornell, frames):
+    """A rect copy on the accumulation stream after per-frame launches (frames = 1) or a fused
+    launch with a 1-frame remainder (9 = 8 fused + 1 per-frame): the copy waits for the main
+    stream's tail, so it holds the finished image, not a half-written one."""
+    W, H = 256, 144
+    r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    r.ctx.set_readback_on_accum_stream(True)
+    dst = r.ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    if frames == 1:
+        for f in (1, 2, 3):
+            r.frame(f, light_bounces=9)
+    else:
+        r.frame(1, n_frames=frames, light_bounces=9)
+    r.ctx.CopyRectToDevicePointer(r.out, 0, W * 16, W * 16, H, dst.device_pointer(), W * 16)
+    got = np.zeros((W * H, 4), np.float32)
+    r.ctx.ReadBuffer(dst, got, blocking=True)
+    want = r.result()
+    dst.release()
+    r.close()
+    assert got.tobytes() == want.tobytes()

@@ -173,9 +173,7 @@ def test_row_tiles_compose_to_full_frame(cornell):
 def test_interleaved_bands_compose_full_frame(cornell, sched):
     """Multi-GPU sharding on one device: period-3 band interleave, each phase launched in
     turn (frames 1 and 2), equals the unsharded render; pack -> unpack round trip too."""
-    import torch
     from clrt import multigpu as mg
-    torch.zeros(1, device="cuda:0")  # initialise torch's HIP context before the library's
     W, H, P = 203, 75, 3
     full = HipRenderer(cornell, W, H, sched=sched)
     for f in (1, 2):
@@ -192,13 +190,13 @@ def test_interleaved_bands_compose_full_frame(cornell, sched):
     import clrt
     dst = r.ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
     for ph in range(P):
-        stage = torch.zeros(mg.staging_bytes(W, H, P) // 4, dtype=torch.float32, device="cuda:0")
-        torch.cuda.synchronize()
+        stage = r.ctx.create_buffer(N.MEM_READ_WRITE, mg.staging_bytes(W, H, P))
         plan = mg.pack_plan(W, H, P, ph)
-        mg.pack_device(r.ctx, r.out, plan, stage.data_ptr())
+        mg.pack_device(r.ctx, r.out, plan, stage.device_pointer())
         r.ctx.Finish()
-        mg.unpack_device(r.ctx, stage.data_ptr(), plan, dst)
+        mg.unpack_device(r.ctx, stage.device_pointer(), plan, dst)
         r.ctx.Finish()
+        stage.release()
     c = np.zeros((W * H, 4), np.float32)
     r.ctx.ReadBuffer(dst, c, blocking=True)
     dst.release()
@@ -285,17 +283,17 @@ def test_large_leaf_uses_global_layout(cornell, oracle_mod):
 
 
 @pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_SHIPPED])
-def test_per_frame_sky_shortcut(cornell, oracle_mod, monkeypatch, math):
-    """Per-frame launches with the sky shortcut forced on (RT_PF_SKY=2; by default it is used
+def test_per_frame_sky_shortcut(cornell, oracle_mod, math):
+    """Per-frame launches with the sky shortcut forced on (perframe_sky 2; by default it is used
     from ~1k pixels per wave): frames 1..6, then a frame with another skybox intensity (the key
     chain no longer matches the stored sky values, so the bit check must fall back to the full
     accumulation), then frames 8..9 -- bit-identical to the shortcut off and, pinned, to the oracle."""
     W, H = 192, 96
     seq = [(f, 1.0) for f in range(1, 7)] + [(7, 1.5)] + [(8, 1.5), (9, 1.0)]
     outs = []
-    for mode in ("2", "0"):
-        monkeypatch.setenv("RT_PF_SKY", mode)
+    for mode in (2, 0):
         r = HipRenderer(cornell, W, H, math=math)
+        r.k.set_tuning("perframe_sky", mode)
         for f, sky in seq:
             r.frame(f, light_bounces=3, skybox=sky)
         outs.append(r.result())

@@ -12,7 +12,6 @@ import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -62,6 +61,7 @@ def _worker(rank, world, port, out_path):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_band_sharded_gather_equals_single_render(tmp_path, cornell, oracle_mod, world):
+    import torch.multiprocessing as mp  # here, not at collection: GPU sessions never load torch
     out = str(tmp_path / "full.npy")
     mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
     got = np.load(out)
