@@ -132,9 +132,13 @@ struct Builder {
     }
 
     static int bucket_of(const Box& cb, const V3& c, unsigned axis) {
-        int b = (int)(kBuckets * cb.rel(c)[(int)axis]);
-        if (b == (int)kBuckets) b = kBuckets - 1;
-        return b;
+        const float x = kBuckets * cb.rel(c)[(int)axis];
+        // finite centroids give x in [0, kBuckets]; a NaN / infinite coordinate (which the
+        // reference would turn into an out-of-range index, undefined behaviour) goes to the
+        // nearest end bucket
+        if (!(x >= 0.0f)) return 0;
+        if (x >= (float)kBuckets) return kBuckets - 1;
+        return (int)x;
     }
 
     BuildNode* build(std::vector<PrimRef>& refs, unsigned s, unsigned e) {
@@ -186,6 +190,18 @@ struct Builder {
                                                 return (unsigned)b <= split;
                                             });
                 mid = (unsigned)(m - &refs[0]);
+                if (mid == s || mid == e) {
+                    // an empty side: impossible for finite centroids (the lowest centroid is
+                    // always in bucket 0), reachable with NaN coordinates -- the reference would
+                    // recurse forever; split at the median instead, NaN ordered last
+                    mid = (s + e) / 2;
+                    auto key = [axis](const PrimRef& r) {
+                        const float c = r.centroid[(int)axis];
+                        return c != c ? std::numeric_limits<float>::infinity() : c;
+                    };
+                    std::nth_element(&refs[s], &refs[mid], &refs[e - 1] + 1,
+                                     [&key](const PrimRef& a, const PrimRef& b) { return key(a) < key(b); });
+                }
             } else {
                 return make_leaf(n, refs, s, e, box);
             }
@@ -525,9 +541,11 @@ int rtsSaveScene(const rt_scene* s, const char* path) {
     if (!f) return RT_INVALID_VALUE;
     bool ok = std::fwrite(kSceneMagic, 1, 8, f) == 8 && std::fwrite(hdr32, sizeof(hdr32), 1, f) == 1 &&
               std::fwrite(hdr64, sizeof(hdr64), 1, f) == 1;
-    ok = ok && std::fwrite(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size(), f) == s->tris.size();
-    ok = ok && std::fwrite(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size(), f) == s->nodes.size();
-    ok = ok && std::fwrite(s->mats.data(), sizeof(rt_cl_material), s->mats.size(), f) == s->mats.size();
+    // (an empty array has no data pointer to hand to fwrite: nothing to write)
+    auto put = [f](const void* p, size_t size, size_t n) { return n == 0 || std::fwrite(p, size, n, f) == n; };
+    ok = ok && put(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size());
+    ok = ok && put(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size());
+    ok = ok && put(s->mats.data(), sizeof(rt_cl_material), s->mats.size());
     ok = ok && std::fwrite(&h, sizeof(h), 1, f) == 1;
     ok = (std::fclose(f) == 0) && ok;
     return ok ? RT_SUCCESS : RT_OUT_OF_RESOURCES;
@@ -561,9 +579,10 @@ int rtsLoadScene(const char* path, rt_scene** out) {
     s->mats.resize(hdr64[2]);
     s->max_prims = hdr32[1];
     uint64_t stored = 0;
-    bool ok = std::fread(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size(), f) == s->tris.size();
-    ok = ok && std::fread(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size(), f) == s->nodes.size();
-    ok = ok && std::fread(s->mats.data(), sizeof(rt_cl_material), s->mats.size(), f) == s->mats.size();
+    auto get = [f](void* p, size_t size, size_t n) { return n == 0 || std::fread(p, size, n, f) == n; };
+    bool ok = get(s->tris.data(), sizeof(rt_cl_triangle), s->tris.size());
+    ok = ok && get(s->nodes.data(), sizeof(rt_cl_bvh_node), s->nodes.size());
+    ok = ok && get(s->mats.data(), sizeof(rt_cl_material), s->mats.size());
     ok = ok && std::fread(&stored, sizeof(stored), 1, f) == 1;
     if (!ok) return RT_PARSE_ERROR;
     uint64_t h = 14695981039346656037ull;

@@ -1,0 +1,230 @@
+// sanitize_main.cpp -- host code under AddressSanitizer + UndefinedBehaviorSanitizer
+// (the OBJ parser's fixed buffers, strtok/sscanf, the SAH builder, the
+// scene cache reader and the CPU oracle are the code a malformed input reaches).
+//
+// Built by `make -C oracle sanitize` (g++/gcc -fsanitize=address,undefined
+// -fno-sanitize-recover=all) from mini-opencl-raytracer_amd/host/{scene,image}.cpp and
+// oracle/rt_oracle.c, run by tests/test_sanitize.py.  Any sanitizer report aborts with a
+// non-zero status.  Inputs:
+//   * OBJ/MTL texts written to a scratch directory: a well-formed quad mesh, n-gons, a face
+//     line longer than the reference's 128-byte buffer, too few / zero / negative /
+//     out-of-range indices, missing "vt", unknown and missing materials, an MTL with
+//     attributes before any newmtl, garbage tokens, empty files, a missing MTL;
+//   * triangle soups for the SAH builder: duplicates, degenerate and coincident triangles,
+//     NaN / infinite coordinates, max primitives 1..8;
+//   * the binary scene cache: round trip, every single-byte corruption of the header, and
+//     truncations;
+//   * the oracle rendering every scene that built (a few pixels, all light types).
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_cl_types.h"
+#include "../../include/rt_image.h"
+#include "../../include/rt_scene.h"
+#include "../../include/rt_status.h"
+
+extern "C" {
+typedef struct {
+    const void* tris;
+    const void* nodes;
+    const void* mats;
+    uint32_t width, height, frameCount;
+    int32_t lightBounces, lightType;
+    float skyboxIntensity;
+    float cam[12];
+} oracle_args;
+int oracle_render_mt(const oracle_args* a, float* result, uint32_t g0, uint32_t g1, int32_t* prim_ids,
+                     float* prim_t, uint64_t* counts4, int threads);
+}
+
+namespace {
+
+std::string g_dir;
+int g_scenes = 0, g_rejected = 0;
+
+void write_file(const std::string& path, const std::string& text) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) {
+        std::perror(path.c_str());
+        std::exit(2);
+    }
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+}
+
+// the reference's traversal keeps a 64-entry stack (kernel_bvh.cl:181): only scenes whose
+// tree fits it are rendered by the oracle, which restates that walk
+void render(const rt_scene* s) {
+    const rt_cl_triangle* t;
+    const rt_cl_bvh_node* n;
+    const rt_cl_material* m;
+    size_t nt, nn, nm;
+    unsigned depth = 0, leaves = 0, maxp = 0;
+    if (rtsGetTriangles(s, &t, &nt) || rtsGetNodes(s, &n, &nn) || rtsGetMaterials(s, &m, &nm)) std::exit(3);
+    if (rtsGetTreeStats(s, &depth, &leaves, &maxp)) std::exit(3);
+    if (nm == 0 || depth >= 60) return;
+    for (size_t i = 0; i < nt; ++i)
+        if (t[i].mtlIndex >= nm) return;  // the GPU path rejects these (rt_capi.cpp prepare_scene)
+    const unsigned W = 17, H = 11;
+    std::vector<float> img(4 * W * H, 0.0f);
+    for (int lt = 0; lt < 3; ++lt) {
+        oracle_args a{t, n, m, W, H, 1u, 5, lt, 1.0f, {0.0f, -25.0f, 8.5f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f}};
+        uint64_t c[4] = {0, 0, 0, 0};
+        oracle_render_mt(&a, img.data(), 0, W * H, nullptr, nullptr, c, 2);
+    }
+    const std::string ppm = g_dir + "/img.ppm";
+    (void)rtiWritePPM(ppm.c_str(), img.data(), W, H);
+}
+
+void cache_roundtrip(const rt_scene* s) {
+    const std::string path = g_dir + "/scene.rtscene";
+    if (rtsSaveScene(s, path.c_str()) != RT_SUCCESS) std::exit(4);
+    rt_scene* back = nullptr;
+    if (rtsLoadScene(path.c_str(), &back) != RT_SUCCESS) std::exit(5);
+    rtsRelease(back);
+    // corrupt every byte of the first 64 (header + counts) and a few in the body; truncate
+    FILE* f = std::fopen(path.c_str(), "rb");
+    std::vector<unsigned char> bytes;
+    int ch;
+    while ((ch = std::fgetc(f)) != EOF) bytes.push_back((unsigned char)ch);
+    std::fclose(f);
+    const std::string bad = g_dir + "/bad.rtscene";
+    for (size_t i = 0; i < bytes.size() && i < 64; ++i) {
+        std::vector<unsigned char> b = bytes;
+        b[i] ^= 0x5a;
+        write_file(bad, std::string(b.begin(), b.end()));
+        rt_scene* x = nullptr;
+        if (rtsLoadScene(bad.c_str(), &x) == RT_SUCCESS) rtsRelease(x);
+    }
+    for (size_t cut : {size_t(0), size_t(7), size_t(31), bytes.size() / 2, bytes.size() - 1}) {
+        write_file(bad, std::string(bytes.begin(), bytes.begin() + (long)std::min(cut, bytes.size())));
+        rt_scene* x = nullptr;
+        if (rtsLoadScene(bad.c_str(), &x) == RT_SUCCESS) rtsRelease(x);
+    }
+}
+
+void try_obj(const char* name, const std::string& obj, const std::string* mtl) {
+    const std::string base = g_dir + "/" + name;
+    write_file(base + ".obj", obj);
+    if (mtl) write_file(base + ".mtl", *mtl);
+    else std::remove((base + ".mtl").c_str());
+    for (unsigned mp = 1; mp <= 5; mp += 2) {
+        rt_scene* s = nullptr;
+        const int rc = rtsLoadOBJ((base + ".obj").c_str(), mp, &s);
+        if (rc != RT_SUCCESS) {
+            ++g_rejected;
+            continue;
+        }
+        ++g_scenes;
+        render(s);
+        cache_roundtrip(s);
+        rtsRelease(s);
+    }
+}
+
+std::string grid_mesh(int n, bool ngons) {
+    std::string o = "mtllib x.mtl\nusemtl white\n";
+    char buf[256];
+    for (int j = 0; j <= n; ++j)
+        for (int i = 0; i <= n; ++i) {
+            std::snprintf(buf, sizeof(buf), "v %f %f %f\n", -5.0 + 10.0 * i / n, 3.0 + 0.3 * std::sin(i + j), -5.0 + 10.0 * j / n);
+            o += buf;
+        }
+    o += "vt 0 0\nvt 1 0\nvt 1 1\nvn 0 -1 0\nvn 0 1 0\n";
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) {
+            const int a = j * (n + 1) + i + 1, b = a + 1, c = a + n + 2, d = a + n + 1;
+            if (ngons) std::snprintf(buf, sizeof(buf), "f %d/1/1 %d/2/1 %d/3/1 %d/1/1\n", a, b, c, d);
+            else std::snprintf(buf, sizeof(buf), "f %d/1/1 %d/2/1 %d/3/1\nf %d/1/1 %d/3/1 %d/2/1\n", a, b, c, a, c, d);
+            o += buf;
+        }
+    return o;
+}
+
+void soups() {
+    std::vector<rt_cl_material> mats(2);
+    std::memset(mats.data(), 0, mats.size() * sizeof(rt_cl_material));
+    mats[0].diffuse = rt_float3{0.7f, 0.7f, 0.7f, 0.0f};
+    mats[0].roughness = 30.0f;
+    mats[1].emission = rt_float3{1.0f, 1.0f, 1.0f, 0.0f};
+    mats[1].roughness = 9999.0f;
+    uint32_t rng = 12345u;
+    auto rnd = [&]() {
+        rng = rng * 1664525u + 1013904223u;
+        return (float)(rng >> 8) / 16777216.0f;
+    };
+    const float specials[] = {0.0f, 1.0f, -1.0f, 1e30f, -1e30f, NAN, INFINITY, -INFINITY, 1e-40f};
+    for (int kind = 0; kind < 6; ++kind)
+        for (unsigned n : {1u, 2u, 3u, 5u, 17u, 200u}) {
+            std::vector<rt_cl_triangle> tris(n);
+            std::memset(tris.data(), 0, n * sizeof(rt_cl_triangle));
+            for (unsigned i = 0; i < n; ++i) {
+                rt_float3* p[3] = {&tris[i].v1.position, &tris[i].v2.position, &tris[i].v3.position};
+                for (int v = 0; v < 3; ++v) {
+                    float x = rnd() * 10 - 5, y = rnd() * 10, z = rnd() * 10 - 5;
+                    if (kind == 1) x = y = z = 1.0f;                         // all coincident
+                    if (kind == 2 && v == 2) { x = p[0]->x; y = p[0]->y; z = p[0]->z; }  // degenerate
+                    if (kind == 3 && i % 3 == 0) x = specials[(i / 3) % 9];  // NaN / inf / huge
+                    if (kind == 4) { x = (float)(i % 4); y = 2.0f; z = 0.0f; }  // duplicates
+                    if (kind == 5) { x = 1e-38f * rnd(); y = 1e-38f; z = -1e-38f; }  // denormal-sized
+                    *p[v] = rt_float3{x, y, z, 0.0f};
+                }
+                tris[i].v1.normal = tris[i].v2.normal = tris[i].v3.normal = rt_float3{0.0f, -1.0f, 0.0f, 0.0f};
+                tris[i].mtlIndex = i % 2;
+            }
+            for (unsigned mp : {1u, 2u, 4u, 8u}) {
+                rt_scene* s = nullptr;
+                if (rtsBuildFromTriangles(tris.data(), n, mats.data(), mats.size(), mp, &s) != RT_SUCCESS) {
+                    ++g_rejected;
+                    continue;
+                }
+                ++g_scenes;
+                render(s);
+                rtsRelease(s);
+            }
+        }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: sanitize_main SCRATCH_DIR\n");
+        return 2;
+    }
+    g_dir = argv[1];
+    const std::string mtl =
+        "Ka 1 1 1\nKd 0.5 0.5 0.5\n"  // attributes before any newmtl
+        "newmtl white\nKd 0.8 0.8 0.8\nKs 0.1 0.1 0.1\nNs 40\nNi 1.5\n"
+        "newmtl light\nKe 5 5 5\nNs 9999\n"
+        "newmtl averyveryveryveryveryveryveryveryveryveryveryveryveryveryveryveryveryveryveryverylongname\nKd 1\n";
+    const std::string light = "usemtl light\n";
+    try_obj("grid", grid_mesh(6, false), &mtl);
+    try_obj("ngons", grid_mesh(5, true), &mtl);
+    try_obj("nomtl", grid_mesh(3, false), nullptr);
+    std::string longface = "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvt 0 0\nvn 0 0 1\nusemtl white\nf";
+    for (int i = 0; i < 40; ++i) longface += (i % 2 ? " 1/1/1" : " 2/1/1") + std::string(i % 3 ? "" : " 3/1/1");
+    longface += "\nf 1/1/1 2/1/1 3/1/1\n";
+    try_obj("longface", longface, &mtl);
+    const char* faces[] = {"f 1/1/1 2/1/1\n", "f 0/1/1 2/1/1 3/1/1\n", "f -1/1/1 2/1/1 3/1/1\n",
+                           "f 1/1/1 2/1/1 99/1/1\n", "f 1/2/1 2/1/1 3/1/1\n", "f 1 2 3\n", "f 1//1 2//1 3//1\n",
+                           "f a b c\n", "f\n", "f 1/1/1 2/1/1 3/1/1 4/1/1 1/1/1 2/1/1 3/1/1\n"};
+    int i = 0;
+    for (const char* f : faces) {
+        const std::string name = "face" + std::to_string(i++);
+        try_obj(name.c_str(), "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvt 0 0\nvn 0 0 1\nusemtl white\n" + light +
+                                  "usemtl nosuch\n" + f, &mtl);
+    }
+    try_obj("garbage", "v 1 2\nvt\nvn x y z\nusemtl\nfoo bar baz\n# comment\n", &mtl);
+    try_obj("empty", "", &mtl);
+    const std::string empty_mtl;
+    try_obj("emptymtl", grid_mesh(2, false), &empty_mtl);
+    soups();
+    std::printf("sanitize: %d scenes built, %d inputs rejected, no sanitizer reports\n", g_scenes, g_rejected);
+    return 0;
+}
