@@ -19,9 +19,11 @@ deterministic (the HIP path is bit-exact with the reference, tests/).
 Roofline of the dominant kernel (KernelEntry's render launch), per launch:
   * bound "valu": the kernel is VALU-issue bound (the Cornell scene lives in LDS; HBM sees the
     output only).  achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU of the
-    same command and build, profiles/pmc.json) / the launch's duration measured live here with
-    HIP events on the kernel's stream; peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-    instruction (MI355X_MICROARCH.md).  frac = achieved / peak.
+    same command and build, profiles/pmc.json) / the launch's time measured live here with HIP
+    events on the kernel's streams (launch_ms: consecutive fused renders overlap, so the interval
+    between their ends, period_ms; kernel_ms is each launch's own event span); peak = 1,024
+    SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md).
+    frac = achieved / peak.
   * lane_util = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU): active lanes per issued VALU op.
   * traffic / hbm_frac: measured HBM bytes per launch ((2 FETCH_SIZE + WRITE_SIZE) KiB, the
     guide's gfx950 correction) and their rate against 8 TB/s.
@@ -220,15 +222,23 @@ def cpu_baseline(scene, args, rays_per_step):
             "ms_per_frame": dt * 1e3 / args.frames}
 
 
-def roofline(args, world, frames_per_launch, kernel_ms, local_counts, tile_px):
+def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts, tile_px):
     alg_bytes = ((48 * local_counts[1] + 48 * local_counts[2] + 164 * local_counts[3]) / args.frames
                  + 32 * tile_px) * frames_per_launch
+    # per-launch time: back-to-back fused renders overlap (one stream per radiance set, each
+    # starts on the CUs the previous one's draining waves free), so a launch's own event span
+    # (kernel_ms) also holds its wait for the previous launch; the interval between the ends of
+    # consecutive launches (period_ms, HIP events on the render streams) is the time each launch
+    # costs -- the denominator here.  Per-frame / unfused launches: the span itself.
+    launch_ms = period_ms if period_ms > 0 else kernel_ms
     rl = {"bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "VALU wave-instructions/s",
-          "frac": None, "traffic": None, "kernel": "KernelEntry", "kernel_ms": round(kernel_ms, 4),
+          "frac": None, "traffic": None, "kernel": "KernelEntry", "launch_ms": round(launch_ms, 4),
+          "kernel_ms": round(kernel_ms, 4), "period_ms": round(period_ms, 4) if period_ms > 0 else None,
           "frames_per_launch": frames_per_launch, "lane_util": None, "hbm_frac": None,
           "alg_bytes_per_launch": int(alg_bytes),
-          "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 2) if kernel_ms > 0 else None,
+          "alg_gbs": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 2) if launch_ms > 0 else None,
           "pmc": None}
+    kernel_ms = launch_ms
     key = workload_key(args, world, frames_per_launch)
     db = json.load(open(PMC_PATH)) if os.path.exists(PMC_PATH) else {}
     e = db.get(key)
@@ -341,7 +351,8 @@ def main():
     launches = max(1, ks["launches"])
     kernel_ms = ks["kernel_ms"] / launches
     frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
-    rl = roofline(args, world, frames_per_launch, kernel_ms, local_counts, r.pixels)
+    period_ms = ks["render_period_ms"] if frames_per_launch > 1 and not args.no_accum_overlap else 0.0
+    rl = roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts, r.pixels)
     rl["accum_overlapped"] = frames_per_launch > 1 and not args.no_accum_overlap
     if not rl["accum_overlapped"] and frames_per_launch > 1:
         rl["accum_ms_per_launch"] = round(ks["accum_ms"] / launches, 4)

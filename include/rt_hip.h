@@ -188,6 +188,10 @@ typedef struct rt_stats {
     uint64_t sched[12];
     double accum_ms;   /* sum of the fused frames' accumulation launches (rtEnqueueKernelFrames);
                         * when overlapped (default) the spans include the wait for the render */
+    double render_period_ms; /* timed renders: mean interval between the ends of consecutive
+                              * launches -- the per-launch time of back-to-back renders, which
+                              * overlap (a launch's event span also holds its wait for the CUs
+                              * the previous one frees) */
 } rt_stats;
 int rtKernelSetStats(rt_kernel k, int enable);
 int rtKernelSetTiming(rt_kernel k, int enable);

@@ -84,7 +84,8 @@ class Stats(ctypes.Structure):
                 ("launches", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
                 ("cycles_refill", ctypes.c_uint64), ("cycles_traverse", ctypes.c_uint64),
                 ("cycles_shade", ctypes.c_uint64), ("cycles_total", ctypes.c_uint64),
-                ("sched", ctypes.c_uint64 * 12), ("accum_ms", ctypes.c_double)]
+                ("sched", ctypes.c_uint64 * 12), ("accum_ms", ctypes.c_double),
+                ("render_period_ms", ctypes.c_double)]
 
 
 class Rect(ctypes.Structure):

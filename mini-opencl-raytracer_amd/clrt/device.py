@@ -218,6 +218,7 @@ class CLKernel:
         check(self._lib.rtKernelGetStats(self.handle, ctypes.byref(s)), "stats")
         return {"rays": s.rays, "node_visits": s.node_visits, "tri_tests": s.tri_tests,
                 "hits": s.hits, "launches": s.launches, "kernel_ms": s.kernel_ms, "accum_ms": s.accum_ms,
+                "render_period_ms": s.render_period_ms,
                 "cycles": {"refill": s.cycles_refill, "traverse": s.cycles_traverse,
                            "shade": s.cycles_shade, "total": s.cycles_total},
                 "sched": dict(zip(("node_steps", "node_lanes", "tri_steps", "tri_lanes", "shade_rounds",

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <limits>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -57,7 +58,7 @@ struct rt_kernel_s {
     uint32_t bulk_percent = 80;                // share of the frame handed out in bulk chunks
                                                // (swept on MI355X: profiles/r01/chunk_sweep.txt)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
-    uint32_t* work_counter = nullptr;  // regen schedule chunk counter
+    uint32_t* work_counter = nullptr;  // persistent schedules' chunk counters: [4] per render stream
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
@@ -71,6 +72,10 @@ struct rt_kernel_s {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_accum;   // fused frames' accumulation
     std::vector<hipEvent_t> event_pool;
     double kernel_ms = 0.0, accum_ms = 0.0;
+    // render period (rt_stats.render_period_ms): ends of consecutive timed renders
+    hipEvent_t first_end = nullptr;
+    double period_span_ms = 0.0;
+    uint64_t period_intervals = 0;
     // fused frames: radiance and primary-miss flag per (frame slot, work-item), two sets used
     // alternately so a render can run while the previous launch's accumulation reads the other
     float4* rad_buf[2] = {};
@@ -175,57 +180,73 @@ void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& sk
 }
 
 // Octant-resolved node records for LDS-resident scenes (stored as 16 planes of float4:
-// A[octant][node], then B[octant][node]): for node n and ray octant o,
+// A[octant][node], then B[octant][node], each plane n + 1 records): for node i and ray
+// octant o,
 //   A = {near.x, near.y, near.z, far.x}, B = {far.y, far.z, hit_next, miss_next}
 // where near/far are the slab planes kernel_bvh.cl:156-169 selects by the ray's signs
-// (bit-exact copies of pmin/pmax), miss_next = skip[n][o] and hit_next is the near child
-// (interior) or the leaf {first, count}: bit 31 set, count-1 in bits 24-29 and first in
-// bits 0-23.  A node step is then two b128 reads, the slab arithmetic and one select.
-// Returns false when a leaf does not fit (> 64 primitives or first >= 2^24): such a
-// scene is rendered from the global layout instead (LDS scenes are small, so this takes
-// an unusual hand-made BVH).
-constexpr uint32_t kLeafBit = 0x80000000u;
+// (bit-exact copies of pmin/pmax), miss_next = skip[i][o] and hit_next is the near child
+// (interior, < 2^24) or the leaf code count << 24 | first (count 1..127).  The reference's
+// "stack empty" is record n, a sentinel every ray misses (its near planes are +inf along the
+// octant's direction, so t0 = +inf) whose successors are n itself: a finished walk parks
+// there, and the kernel needs no end test per step.  A node step is two b128 reads, the slab
+// arithmetic and two selects.  Returns false when a leaf does not fit (> 127 primitives or
+// first + count > 2^24): such a scene is rendered from the global layout instead (LDS scenes
+// are small, so this takes an unusual hand-made BVH).
+constexpr uint32_t kLeafMin = 1u << 24;
 
 bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
                      std::vector<uint32_t>& out) {
-    out.assign((size_t)n * 8 * 8, 0u);
-    bool ok = true;
+    const uint32_t stride = n + 1;
+    out.assign((size_t)stride * 8 * 8, 0u);
+    bool ok = n < kLeafMin;
     auto bits = [](float f) {
         uint32_t u;
         std::memcpy(&u, &f, 4);
         return u;
     };
-    for (uint32_t i = 0; i < n; ++i) {
-        const rt_cl_bvh_node& x = nd[i];
+    const float inf = std::numeric_limits<float>::infinity();
+    for (uint32_t i = 0; i <= n; ++i) {
         uint32_t leaf = 0;
-        if (x.nPrimitives > 0) {
-            if (x.offset < (1u << 24) && x.nPrimitives <= 64)
-                leaf = kLeafBit | ((uint32_t)(x.nPrimitives - 1) << 24) | x.offset;
-            else
-                ok = false;
+        float lo[3], hi[3];
+        if (i < n) {
+            const rt_cl_bvh_node& x = nd[i];
+            if (x.nPrimitives > 0) {
+                if (x.nPrimitives <= 127 && (uint64_t)x.offset + x.nPrimitives <= kLeafMin)
+                    leaf = ((uint32_t)x.nPrimitives << 24) | x.offset;
+                else
+                    ok = false;
+            }
+            lo[0] = x.bounds.pmin.x, lo[1] = x.bounds.pmin.y, lo[2] = x.bounds.pmin.z;
+            hi[0] = x.bounds.pmax.x, hi[1] = x.bounds.pmax.y, hi[2] = x.bounds.pmax.z;
+        } else {
+            // END sentinel: near plane +inf (octant bit clear: near = pmin) or -inf (set: near =
+            // pmax), i.e. lo = +inf, hi = -inf -- (near - o) * invDir = +inf on every axis
+            for (int ax = 0; ax < 3; ++ax) lo[ax] = inf, hi[ax] = -inf;
         }
-        const float lo[3] = {x.bounds.pmin.x, x.bounds.pmin.y, x.bounds.pmin.z};
-        const float hi[3] = {x.bounds.pmax.x, x.bounds.pmax.y, x.bounds.pmax.z};
         for (uint32_t o = 0; o < 8; ++o) {
             // octant-major planes A[o][node], B[o][node] (16 B each): lanes visiting different
             // nodes in the same octant hit different LDS banks
-            uint32_t* ra = &out[((size_t)o * n + i) * 4];
-            uint32_t* rb = &out[((size_t)(8 + o) * n + i) * 4];
-            uint32_t* r[8] = {ra, ra + 1, ra + 2, ra + 3, rb, rb + 1, rb + 2, rb + 3};
+            uint32_t* ra = &out[((size_t)o * stride + i) * 4];
+            uint32_t* rb = &out[((size_t)(8 + o) * stride + i) * 4];
             float nr[3], fr[3];
             for (int ax = 0; ax < 3; ++ax) {
                 const bool neg = (o >> ax) & 1u;
                 nr[ax] = neg ? hi[ax] : lo[ax];
                 fr[ax] = neg ? lo[ax] : hi[ax];
             }
-            *r[0] = bits(nr[0]);
-            *r[1] = bits(nr[1]);
-            *r[2] = bits(nr[2]);
-            *r[3] = bits(fr[0]);
-            *r[4] = bits(fr[1]);
-            *r[5] = bits(fr[2]);
-            *r[6] = x.nPrimitives > 0 ? leaf : (((o >> x.axis) & 1u) ? x.offset : i + 1);
-            *r[7] = skips[(size_t)i * 8 + o];
+            ra[0] = bits(nr[0]);
+            ra[1] = bits(nr[1]);
+            ra[2] = bits(nr[2]);
+            ra[3] = bits(fr[0]);
+            rb[0] = bits(fr[1]);
+            rb[1] = bits(fr[2]);
+            if (i == n) {
+                rb[2] = rb[3] = n;
+                continue;
+            }
+            const uint32_t skip = skips[(size_t)i * 8 + o];
+            rb[2] = nd[i].nPrimitives > 0 ? leaf : (((o >> nd[i].axis) & 1u) ? nd[i].offset : i + 1);
+            rb[3] = skip == 0xffffffffu ? n : skip;
         }
     }
     return ok;
@@ -340,7 +361,7 @@ int prepare_scene(rt_kernel k) {
     }
     std::vector<uint32_t> oct;
     const bool oct_ok = build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct);
-    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)nn * 16);
+    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)(nn + 1) * 16);
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
@@ -391,13 +412,29 @@ hipEvent_t take_event(rt_kernel k) {
     return e;
 }
 
-static int drain_list(rt_kernel k, std::vector<std::pair<hipEvent_t, hipEvent_t>>& list, double& total) {
+static int drain_list(rt_kernel k, std::vector<std::pair<hipEvent_t, hipEvent_t>>& list, double& total,
+                      bool renders) {
     for (auto& pr : list) {
         float ms = 0.0f;
         hipError_t e = hipEventSynchronize(pr.second);
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, pr.first, pr.second);
         if (e != hipSuccess) return map_hip(e);
         total += ms;
+        if (renders) {
+            // render period: end of the first timed render to end of the latest one
+            if (!k->first_end) {
+                k->first_end = pr.second;
+            } else {
+                float span = 0.0f;
+                e = hipEventElapsedTime(&span, k->first_end, pr.second);
+                if (e != hipSuccess) return map_hip(e);
+                k->period_span_ms = span;
+                ++k->period_intervals;
+                k->event_pool.push_back(pr.second);
+            }
+            k->event_pool.push_back(pr.first);
+            continue;
+        }
         k->event_pool.push_back(pr.first);
         k->event_pool.push_back(pr.second);
     }
@@ -406,9 +443,16 @@ static int drain_list(rt_kernel k, std::vector<std::pair<hipEvent_t, hipEvent_t>
 }
 
 int drain_events(rt_kernel k) {
-    int rc = drain_list(k, k->pending_events, k->kernel_ms);
+    int rc = drain_list(k, k->pending_events, k->kernel_ms, true);
     if (rc) return rc;
-    return drain_list(k, k->pending_accum, k->accum_ms);
+    return drain_list(k, k->pending_accum, k->accum_ms, false);
+}
+
+void reset_period(rt_kernel k) {
+    if (k->first_end) k->event_pool.push_back(k->first_end);
+    k->first_end = nullptr;
+    k->period_span_ms = 0.0;
+    k->period_intervals = 0;
 }
 
 }  // namespace
@@ -428,12 +472,16 @@ int rtCreateContext(int device_index, rt_context* out) {
     c->device = device_index;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->astream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream[0], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream[1], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->atail, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->mtail, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->gtail, hipEventDisableTiming);
     if (e != hipSuccess) {
         if (c->stream) (void)hipStreamDestroy(c->stream);
         if (c->astream) (void)hipStreamDestroy(c->astream);
+        for (hipStream_t r : c->rstream)
+            if (r) (void)hipStreamDestroy(r);
         delete c;
         return RT_INVALID_COMMAND_QUEUE;
     }
@@ -451,6 +499,10 @@ int rtReleaseContext(rt_context ctx) {
     (void)hipStreamSynchronize(ctx->astream);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->astream);
+    for (hipStream_t r : ctx->rstream) {
+        (void)hipStreamSynchronize(r);
+        (void)hipStreamDestroy(r);
+    }
     (void)hipEventDestroy(ctx->atail);
     (void)hipEventDestroy(ctx->mtail);
     (void)hipEventDestroy(ctx->gtail);
@@ -521,7 +573,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16);
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 32);
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
     if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
@@ -551,6 +603,7 @@ int rtReleaseKernel(rt_kernel k) {
         if (k->rad_free[i]) (void)hipEventDestroy(k->rad_free[i]);
     }
     if (k->render_done) (void)hipEventDestroy(k->render_done);
+    if (k->first_end) (void)hipEventDestroy(k->first_end);
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
@@ -657,6 +710,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.shadeMats = k->shade_mats + (k->math == RT_MATH_SHIPPED ? 4 * (size_t)k->n_mats : 0);
     a.nMats = k->n_mats;
     a.nNodes = k->n_nodes;
+    a.octStride = k->n_nodes + 1;
     a.nTris = k->n_tris;
     a.width = W;
     a.height = H;
@@ -700,6 +754,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.nFrames = n_frames;
     a.radStride = (uint32_t)g1;
     a.radBuf = nullptr;
+    hipStream_t rstr = ctx->stream;  // the stream this launch's render goes to
     if (n_frames > 1) {
         // fused frames: radiance slots indexed by global work-item id (the lane packs
         // slot * g1 + gid into 32 bits); tiles x frames work items
@@ -725,14 +780,26 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (me != hipSuccess) return map_hip(me);
             k->rad_buf_cap[rs] = need;
         }
+        if (ctx->overlap && !k->hit_ids) {
+            // the set's own render stream, after everything queued on the main stream so far
+            // (buffer writes, per-frame launches) but not after the previous step's render or
+            // accumulation: it fills the CUs that render's draining waves free.  (With hit
+            // buffers bound the renders stay in order on the main stream: each writes them.)
+            rstr = ctx->rstream[rs];
+            hipError_t me = hipEventRecord(ctx->mtail, ctx->stream);
+            if (me == hipSuccess) me = hipStreamWaitEvent(rstr, ctx->mtail, 0);
+            if (me != hipSuccess) return map_hip(me);
+        }
         // the render writes the set: after the accumulation that last read it
         if (k->rad_busy[rs]) {
-            hipError_t me = hipStreamWaitEvent(ctx->stream, k->rad_free[rs], 0);
+            hipError_t me = hipStreamWaitEvent(rstr, k->rad_free[rs], 0);
             if (me != hipSuccess) return map_hip(me);
             k->rad_busy[rs] = false;
         }
         a.radBuf = k->rad_buf[rs];
         a.frameFlags = k->frame_flags[rs];
+        // one chunk counter per radiance set: renders of the two sets may run together
+        a.workCounter = k->work_counter + 4 * rs;
     }
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
@@ -740,7 +807,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
     // (48 B per triangle, 64 B per material); no stack
-    const size_t scene_bytes = (size_t)k->n_nodes * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
+    const size_t scene_bytes = (size_t)(k->n_nodes + 1) * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.refillMin = lds ? k->refill_min : k->refill_min_g;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g;
@@ -782,7 +849,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
     }
     if (k->sched != RT_SCHED_TILES) {
-        hipError_t me = hipMemsetAsync(k->work_counter, 0, 16, ctx->stream);
+        hipError_t me = hipMemsetAsync(a.workCounter, 0, 16, rstr);
         if (me != hipSuccess) return map_hip(me);
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -790,12 +857,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         ev0 = take_event(k);
         ev1 = take_event(k);
         if (!ev0 || !ev1) return RT_OUT_OF_RESOURCES;
-        (void)hipEventRecord(ev0, ctx->stream);
+        (void)hipEventRecord(ev0, rstr);
     }
-    hipError_t e = rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, ctx->stream);
+    hipError_t e = rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, rstr);
     if (e != hipSuccess) return map_hip(e);
     if (k->timing) {
-        (void)hipEventRecord(ev1, ctx->stream);
+        (void)hipEventRecord(ev1, rstr);
         k->pending_events.emplace_back(ev0, ev1);
     }
     if (a.pfKeyIn) k->pf_parity ^= 1;
@@ -806,7 +873,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         hipStream_t as = ctx->stream;
         if (ctx->overlap) {
             as = ctx->astream;
-            e = hipEventRecord(k->render_done, ctx->stream);
+            e = hipEventRecord(k->render_done, rstr);
             if (e == hipSuccess) e = hipStreamWaitEvent(as, k->render_done, 0);
             if (e != hipSuccess) return map_hip(e);
         }
@@ -1034,6 +1101,7 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     out->launches = k->launches;
     out->kernel_ms = k->kernel_ms;
     out->accum_ms = k->accum_ms;
+    out->render_period_ms = k->period_intervals ? k->period_span_ms / (double)k->period_intervals : 0.0;
     return RT_SUCCESS;
 }
 
@@ -1046,6 +1114,7 @@ int rtKernelResetStats(rt_kernel k) {
     k->launches = 0;
     k->kernel_ms = 0.0;
     k->accum_ms = 0.0;
+    reset_period(k);
     hipError_t e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(k->ctx));
     if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
     return map_hip(e);

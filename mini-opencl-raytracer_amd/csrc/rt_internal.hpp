@@ -20,6 +20,10 @@ struct rt_context_s {
     // accumulations enqueued so far -- to the caller the context stays one in-order queue.
     hipStream_t astream = nullptr;
     hipEvent_t atail = nullptr;  // last accumulation enqueued on astream
+    // fused renders alternate between two streams, one per radiance set (rt_capi.cpp enqueue):
+    // renders of consecutive steps are independent, so step k+1's waves take the CUs that step
+    // k's draining waves free instead of waiting for its last path
+    hipStream_t rstream[2] = {};
     hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
     bool apending = false;
     bool overlap = true;  // rtContextSetAccumOverlap(ctx, 0): accumulate on the main stream

@@ -127,13 +127,13 @@ __global__ void accum_key(KernelArgs a, uint32_t* key) {
 
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st) {
     if (math == MathShipped::kId) return launch_accum_frames_shipped(a, key, st);
-    const dim3 grid((a.nTiles + 4u * kAccumTilesPerWave - 1u) / (4u * kAccumTilesPerWave));
+    const dim3 grid((a.nTiles + kAccumWgWaves * kAccumTilesPerWave - 1u) / (kAccumWgWaves * kAccumTilesPerWave));
     if (math == MathDeviceLib::kId) {
         hipLaunchKernelGGL(accum_key<MathDeviceLib>, dim3(1), dim3(64), 0, st, a, key);
-        hipLaunchKernelGGL(accum_frames<MathDeviceLib>, grid, dim3(256), 0, st, a, key);
+        hipLaunchKernelGGL(accum_frames<MathDeviceLib>, grid, dim3(64 * kAccumWgWaves), 0, st, a, key);
     } else {
         hipLaunchKernelGGL(accum_key<MathPinned>, dim3(1), dim3(64), 0, st, a, key);
-        hipLaunchKernelGGL(accum_frames<MathPinned>, grid, dim3(256), 0, st, a, key);
+        hipLaunchKernelGGL(accum_frames<MathPinned>, grid, dim3(64 * kAccumWgWaves), 0, st, a, key);
     }
     return hipGetLastError();
 }

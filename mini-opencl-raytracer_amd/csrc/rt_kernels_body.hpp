@@ -121,8 +121,11 @@ struct SceneView {
     const float4* smats;    // per material: {diffuse, 1/(alpha+1)}, {specular, alpha^2/pi}, {emission, alpha^2-1}, {roughness, alpha, -, -}
 };
 
-constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished
-constexpr uint32_t kLeafBit = 0x80000000u;  // octant record hit_next: leaf {first, count}
+constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished (global node records)
+// Octant records (LDS scenes): hit_next is the near child (< 2^24) or a leaf code
+// count << 24 | first (count 1..127); the walk's END is a sentinel record at index nNodes that
+// every ray misses and whose successors are itself (rt_capi.cpp, build_oct_nodes).
+constexpr uint32_t kLeafMin = 1u << 24;
 
 // Scene into LDS once per workgroup (when it fits), else read in place.
 template <bool kLdsScene>
@@ -131,10 +134,10 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     if (kLdsScene) {
         const int tid = threadIdx.x;
         float4* lo = smem;
-        float4* lt = lo + 16 * a.nNodes;
+        float4* lt = lo + 16 * a.octStride;
         float4* ls = lt + 3 * a.nTris;
         float4* lm = ls + 3 * a.nTris;
-        for (uint32_t i = tid; i < 16 * a.nNodes; i += 256) lo[i] = a.octNodes[i];
+        for (uint32_t i = tid; i < 16 * a.octStride; i += 256) lo[i] = a.octNodes[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
         for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
@@ -151,7 +154,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kLdsScene ? 16u * a.nNodes + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
+    return kLdsScene ? 16u * a.octStride + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -185,8 +188,8 @@ template <bool kOct>
 __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
                                            float t, uint32_t& next, uint32_t& first, uint32_t& count) {
     if (kOct) {
-        const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
-        const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
+        const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+        const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.octStride];
         float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
         float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
         t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
@@ -195,10 +198,10 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
         t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
         const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
         const bool hit = t1 >= t0;
-        const bool leaf = hit && (hn & kLeafBit);
+        const bool leaf = hit && hn >= kLeafMin;
         next = (hit && !leaf) ? hn : mn;
         first = hn & 0x00ffffffu;
-        count = ((hn >> 24) & 0x3fu) + 1u;
+        count = hn >> 24;
         return leaf;
     }
     // global 64-B record; the first nTop records are read from their LDS copy (one flat load
@@ -223,8 +226,8 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
 // LDS octant record visit returning the raw hit_next word on entering a leaf.
 __device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
                                           float t, uint32_t& next, uint32_t& leaf_code) {
-    const uint32_t i = __umul24(r.sgn, a.nNodes) + cur;
-    const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.nNodes];
+    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+    const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.octStride];
     float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
     float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
     t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
@@ -233,7 +236,7 @@ __device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs&
     t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
     const uint32_t hn = __float_as_uint(B.z), mn = __float_as_uint(B.w);
     const bool hit = t1 >= t0;
-    const bool leaf = hit && (hn & kLeafBit);
+    const bool leaf = hit && hn >= kLeafMin;
     next = (hit && !leaf) ? hn : mn;
     leaf_code = hn;
     return leaf;
@@ -301,7 +304,8 @@ __device__ __forceinline__ Traversal intersect(const SceneView& sc, const Kernel
                                                uint32_t& visits, uint32_t& tests) {
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
     uint32_t cur = 0;
-    while (cur != kEnd) {
+    const uint32_t end = kOct ? a.nNodes : kEnd;
+    while (cur != end) {
         if (kStats) ++visits;
         uint32_t next, first = 0, count = 0;
         if (node_visit<kOct>(sc, a, cur, r, h.t, next, first, count)) {
@@ -692,6 +696,7 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
 // at once.  Per lane the sequence of node visits and triangle tests -- and therefore every
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
+constexpr uint32_t kNotWalking = 0x80000000u;  // LDS path walk word outside TRAV
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -810,7 +815,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
     uint32_t cur = 0;  // TRAV: node to visit; LEAF: node to continue at after the leaf
-    uint32_t leaf_i = 0, leaf_end = 0;
+    // LDS path: the walk word (see the node steps), kNotWalking outside TRAV; global path: the
+    // leaf's next triangle
+    uint32_t leaf_i = kLdsScene ? kNotWalking : 0u, leaf_end = 0;
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
@@ -933,6 +940,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         state = kTrav;
                         h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                         cur = 0;
+                        if (kLdsScene) leaf_i = 0u;  // walking, at the root
                         if (kStats) ++st.rays;
                     } else {
                         state = kDone;  // no bounce: radiance max(0, 0) = 0
@@ -992,6 +1000,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                             cur = 0;
+                            if (kLdsScene) leaf_i = 0u;  // walking, at the root
                             if (kStats) ++st.rays;
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
@@ -1025,8 +1034,20 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         // instruction (weights ~ the two bodies' VALU cost), so the wave never pays both
         // bodies for a mix of lanes.
         for (;;) {
-            const uint32_t n_trav = popc_ballot(state == kTrav);
-            const uint32_t n_leaf = popc_ballot(state == kLeaf);
+            uint32_t n_trav, n_leaf;
+            if (kLdsScene) {
+                // a walk parked on the END sentinel has finished the reference's traversal
+                // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
+                if (leaf_i < kLeafMin && cur == a.nNodes) {
+                    state = kShade;
+                    leaf_i = kNotWalking;
+                }
+                n_trav = popc_ballot(leaf_i < kLeafMin);
+                n_leaf = popc_ballot((int32_t)leaf_i >= (int32_t)kLeafMin);
+            } else {
+                n_trav = popc_ballot(state == kTrav);
+                n_leaf = popc_ballot(state == kLeaf);
+            }
             if (n_trav + n_leaf == 0u) break;
             if (popc_ballot(state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
@@ -1048,18 +1069,21 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (!leaf_step) {
 #pragma unroll
                 for (int rep = 0; rep < kNodeBurst; ++rep) {
-                    if (state == kTrav) {
+                    if (kLdsScene) {
+                        // walk word (LDS path): < 2^24 = at node `cur`; a passed leaf stores its
+                        // code count << 24 | first, which the triangle steps count down; a walk
+                        // that reached END keeps visiting the sentinel (always missed, its own
+                        // successor) until the next decision -- no per-step end test
+                        if (leaf_i < kLeafMin) {
+                            if (kStats && cur != a.nNodes) ++st.visits;
+                            uint32_t next, code;
+                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) leaf_i = code;
+                            cur = next;
+                        }
+                    } else if (state == kTrav) {
                         if (kStats) ++st.visits;
                         uint32_t next, first = 0, count = 0;
-                        if (kLdsScene) {
-                            // LDS records: the LEAF state keeps the packed leaf word itself
-                            // (bit 31 | count-1 << 24 | first); the triangle steps walk it
-                            uint32_t code;
-                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
-                                state = kLeaf;
-                                leaf_i = code;
-                            }
-                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
+                        if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
                             state = kLeaf;
                             leaf_i = first;
                             leaf_end = first + count;
@@ -1071,18 +1095,20 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             } else {
 #pragma unroll
                 for (int rep = 0; rep < kTriBurst; ++rep) {
-                    if (state == kLeaf) {
-                        if (kStats) ++st.tests;
-                        if (kLdsScene) {
+                    if (kLdsScene) {
+                        // one triangle of the leaf; the last one drops the word below 2^24
+                        // (first + count), so the lane is back at node `cur` = the skip pointer
+                        if ((int32_t)leaf_i >= (int32_t)kLeafMin) {
+                            if (kStats) ++st.tests;
                             const uint32_t idx = leaf_i & 0x00ffffffu;
                             ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kShade : kTrav;
-                            leaf_i += 1u - (1u << 24);
-                        } else {
-                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                            ++leaf_i;
-                            if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
+                            leaf_i += 1u - kLeafMin;
                         }
+                    } else if (state == kLeaf) {
+                        if (kStats) ++st.tests;
+                        ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                        ++leaf_i;
+                        if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
                     }
                 }
             }
@@ -1117,6 +1143,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 state = kTrav;
                 h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                 cur = 0;
+                if (kLdsScene) leaf_i = 0u;  // walking, at the root
                 if (kStats) ++st.rays;
             }
         }
@@ -1522,7 +1549,7 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                             leaf_end = first + count;
                         }
                         cur = next;
-                        if (state == kTrav && next == kEnd) state = kFin;
+                        if (state == kTrav && next == (kLdsScene ? a.nNodes : kEnd)) state = kFin;
                     }
                 }
             } else {
@@ -1533,8 +1560,8 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
                         if (kLdsScene) {
                             const uint32_t idx = leaf_i & 0x00ffffffu;
                             ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            if ((leaf_i & 0x3f000000u) == 0u) state = cur == kEnd ? kFin : kTrav;
-                            leaf_i += 1u - (1u << 24);
+                            if ((leaf_i >> 24) == 1u) state = cur == a.nNodes ? kFin : kTrav;
+                            leaf_i += 1u - kLeafMin;
                         } else {
                             ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
                             ++leaf_i;
@@ -1662,17 +1689,21 @@ __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* ke
 #define RT_ACCUM_TPW 1
 #endif
 constexpr uint32_t kAccumTilesPerWave = RT_ACCUM_TPW;  // 8x8 tiles per wave of the accumulation launch
+#ifndef RT_ACCUM_WG_WAVES
+#define RT_ACCUM_WG_WAVES 4
+#endif
+constexpr uint32_t kAccumWgWaves = RT_ACCUM_WG_WAVES;  // waves per accumulation workgroup
 constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
 
 template <class M>
 __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uint32_t* key) {
-    __shared__ uint32_t queue[4][kAccumQueue];
+    __shared__ uint32_t queue[kAccumWgWaves][kAccumQueue];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t* q = queue[wv];
     uint32_t qn = 0;  // wave-uniform
     const uint32_t kold = key[2], kout = key[3];
     const float krf = __uint_as_float(key[1]);
-    const uint32_t tile0 = (blockIdx.x * 4u + wv) * kAccumTilesPerWave;
+    const uint32_t tile0 = (blockIdx.x * kAccumWgWaves + wv) * kAccumTilesPerWave;
     for (uint32_t t = 0; t < kAccumTilesPerWave; ++t) {
         const uint32_t tile = tile0 + t;
         if (tile >= a.nTiles) break;  // wave-uniform

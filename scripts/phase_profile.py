@@ -25,7 +25,8 @@ for name in scheds:
   for math in maths:
     for lb in lbs:
         r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=sched)
-        r.frame(1, light_bounces=lb)
+        nf = int(os.environ.get("RT_PHASE_FRAMES", "8"))
+        r.frame(1, light_bounces=lb, n_frames=nf if nf > 1 else None)
         r.ctx.Finish()
         s = r.k.stats()
         c = s["cycles"]

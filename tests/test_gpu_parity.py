@@ -256,25 +256,26 @@ def test_malformed_bvh_is_rejected_not_run(cornell):
     r.close()
 
 
-def test_large_leaf_uses_global_layout(cornell, oracle_mod):
-    """A root-only BVH -- one leaf holding all 72 triangles, more than the LDS node records
-    encode inline (64) -- is rendered from the global layout; bit-exact against the oracle."""
+@pytest.mark.parametrize("n_tris,in_lds", [(100, True), (144, False)])
+def test_large_leaf_layouts(cornell, oracle_mod, n_tris, in_lds):
+    """A root-only BVH whose one leaf holds n_tris triangles (Cornell's, repeated): up to 127
+    fit the LDS node records' inline leaf code, more are rendered from the global layout;
+    bit-exact against the oracle either way."""
     import dataclasses
-    tris = cornell.triangles
+    tris = np.concatenate([cornell.triangles, cornell.triangles])[:n_tris]
     p = np.concatenate([tris["v1"]["position"], tris["v2"]["position"], tris["v3"]["position"]])[:, :3]
     root = np.zeros(1, N.NODE_DTYPE)
     root["bmin"][0, :3] = p.min(0)
     root["bmax"][0, :3] = p.max(0)
     root["nPrimitives"] = len(tris)
-    assert len(tris) > 64
-    sc = dataclasses.replace(cornell, nodes=root)
+    sc = dataclasses.replace(cornell, triangles=tris, nodes=root)
     W, H = 96, 64
     r = HipRenderer(sc, W, H, hits=True, stats=True)
     r.frame(1, light_bounces=4)
     got = r.result()
     ids, _ = r.hits()
     st = r.k.stats()
-    assert not r.k.scene_in_lds()
+    assert r.k.scene_in_lds() == in_lds
     r.close()
     want, wids, _, c = _oracle(oracle_mod, sc, W, H, [1], 4, hits=True)
     assert np.array_equal(ids, wids)
