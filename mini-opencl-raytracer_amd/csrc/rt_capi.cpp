@@ -194,9 +194,15 @@ void build_skips(const rt_cl_bvh_node* nd, uint32_t n, std::vector<uint32_t>& sk
 // are small, so this takes an unusual hand-made BVH).
 constexpr uint32_t kLeafMin = 1u << 24;
 
+// records per octant plane: the n nodes, the END sentinel, and one pad record when that count is
+// even -- an odd plane stride (x 16 B) staggers the eight planes over the LDS banks, so lanes of
+// different octants at the same node do not collide (an even stride of 40 put planes o and o+2
+// on the same banks: +40 % bank-conflict cycles)
+inline uint32_t oct_stride(uint32_t n) { return (n + 1) | 1u; }
+
 bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
                      std::vector<uint32_t>& out) {
-    const uint32_t stride = n + 1;
+    const uint32_t stride = oct_stride(n);
     out.assign((size_t)stride * 8 * 8, 0u);
     bool ok = n < kLeafMin;
     auto bits = [](float f) {
@@ -361,7 +367,7 @@ int prepare_scene(rt_kernel k) {
     }
     std::vector<uint32_t> oct;
     const bool oct_ok = build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct);
-    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)(nn + 1) * 16);
+    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)oct_stride(nn) * 16);
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
@@ -710,7 +716,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.shadeMats = k->shade_mats + (k->math == RT_MATH_SHIPPED ? 4 * (size_t)k->n_mats : 0);
     a.nMats = k->n_mats;
     a.nNodes = k->n_nodes;
-    a.octStride = k->n_nodes + 1;
+    a.octStride = oct_stride(k->n_nodes);
     a.nTris = k->n_tris;
     a.width = W;
     a.height = H;
@@ -807,7 +813,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
     // (48 B per triangle, 64 B per material); no stack
-    const size_t scene_bytes = (size_t)(k->n_nodes + 1) * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
+    const size_t scene_bytes = (size_t)oct_stride(k->n_nodes) * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.refillMin = lds ? k->refill_min : k->refill_min_g;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g;

@@ -20,7 +20,7 @@ struct KernelArgs {
     const float4* shadeTris;            // derived from slot 1: {n1, mtlIndex}, {n2, n3.x}, {n3.yz} per triangle
     const float4* shadeMats;            // derived from slot 3: {diffuse, 1/(a+1)}, {specular, a^2/pi}, {emission, a^2-1}, {rough, a}
     uint32_t nNodes, nTris, nMats;
-    uint32_t octStride;                 // LDS path: records per octant plane = nNodes + 1 (END sentinel)
+    uint32_t octStride;                 // LDS path: records per octant plane (nodes, END sentinel, odd pad)
     uint32_t nTop;                      // global path: leading gNodes records staged in LDS
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)

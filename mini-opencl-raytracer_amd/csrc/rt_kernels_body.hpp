@@ -738,6 +738,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
 #endif
+
 // the same for scenes read from HBM/L2 (global path)
 #ifndef RT_GNODE_BURST
 #define RT_GNODE_BURST RT_NODE_BURST
