@@ -101,8 +101,8 @@ struct rt_kernel_s {
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[rtk::kNumSched][3][2][2] = {};  // [sched][math][lds][stats] -> blocks per CU (0 = unknown)
-    size_t occ_smem[rtk::kNumSched][3][2][2] = {};
+    int occ_cache[rtk::kNumSched][3][2][2][2] = {};  // [sched][math][lds][stats][bofs] -> blocks per CU (0 = unknown)
+    size_t occ_smem[rtk::kNumSched][3][2][2][2] = {};
 };
 
 namespace {
@@ -199,11 +199,17 @@ constexpr uint32_t kLeafMin = 1u << 24;
 // different octants at the same node do not collide (an even stride of 40 put planes o and o+2
 // on the same banks: +40 % bank-conflict cycles)
 inline uint32_t oct_stride(uint32_t n) { return (n + 1) | 1u; }
+// float4 offset of the B planes: rtk::kOctB for trees of at most kOctBMaxStride records per plane
+// (a node step then reads B at an immediate offset from A), else right after the A planes
+inline uint32_t oct_b(uint32_t n) {
+    return oct_stride(n) <= rtk::kOctBMaxStride ? rtk::kOctB : 8u * oct_stride(n);
+}
+inline uint32_t oct_records(uint32_t n) { return oct_b(n) + 8u * oct_stride(n); }
 
 bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uint32_t>& skips,
                      std::vector<uint32_t>& out) {
-    const uint32_t stride = oct_stride(n);
-    out.assign((size_t)stride * 8 * 8, 0u);
+    const uint32_t stride = oct_stride(n), bofs = oct_b(n);
+    out.assign((size_t)oct_records(n) * 4, 0u);
     bool ok = n < kLeafMin;
     auto bits = [](float f) {
         uint32_t u;
@@ -233,7 +239,7 @@ bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
             // octant-major planes A[o][node], B[o][node] (16 B each): lanes visiting different
             // nodes in the same octant hit different LDS banks
             uint32_t* ra = &out[((size_t)o * stride + i) * 4];
-            uint32_t* rb = &out[((size_t)(8 + o) * stride + i) * 4];
+            uint32_t* rb = &out[((size_t)bofs + (size_t)o * stride + i) * 4];
             float nr[3], fr[3];
             for (int ax = 0; ax < 3; ++ax) {
                 const bool neg = (o >> ax) & 1u;
@@ -367,7 +373,7 @@ int prepare_scene(rt_kernel k) {
     }
     std::vector<uint32_t> oct;
     const bool oct_ok = build_oct_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, skips, oct);
-    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)oct_stride(nn) * 16);
+    rc = ensure_dev(k->oct_nodes, k->oct_nodes_cap, (size_t)oct_records(nn));
     if (rc) return rc;
     {
         hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
@@ -717,6 +723,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.nMats = k->n_mats;
     a.nNodes = k->n_nodes;
     a.octStride = oct_stride(k->n_nodes);
+    a.octB = oct_b(k->n_nodes);
+    a.octRecords = oct_records(k->n_nodes);
     a.nTris = k->n_tris;
     a.width = W;
     a.height = H;
@@ -813,7 +821,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
     // (48 B per triangle, 64 B per material); no stack
-    const size_t scene_bytes = (size_t)oct_stride(k->n_nodes) * 256 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
+    const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
     a.refillMin = lds ? k->refill_min : k->refill_min_g;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g;
@@ -825,10 +833,11 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     const int mi = k->math;
     const int si = k->sched;
-    int& occ = k->occ_cache[si][mi][lds][k->stats];
-    if (occ == 0 || k->occ_smem[si][mi][lds][k->stats] != smem) {
-        occ = rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, smem);
-        k->occ_smem[si][mi][lds][k->stats] = smem;
+    const bool bofs = lds && a.octB == rtk::kOctB;
+    int& occ = k->occ_cache[si][mi][lds][k->stats][bofs];
+    if (occ == 0 || k->occ_smem[si][mi][lds][k->stats][bofs] != smem) {
+        occ = rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem);
+        k->occ_smem[si][mi][lds][k->stats][bofs] = smem;
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave

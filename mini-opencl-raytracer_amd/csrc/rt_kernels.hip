@@ -11,10 +11,10 @@ namespace rtk {
 // 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
 // (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
 // (LDS scenes 5 waves per SIMD, scenes read from HBM/L2 6, as for the shipped policy)
-template <bool kStats>
+template <bool kStats, bool kBofs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
 void kernel_entry_step_devicelib_lds(KernelArgs a) {
-    step_body<MathDeviceLib, true, kStats>(a);
+    step_body<MathDeviceLib, true, kStats, kBofs>(a);
 }
 template <bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
@@ -26,9 +26,9 @@ void kernel_entry_step_devicelib_global(KernelArgs a) {
 #else
 #define RT_STEP_PINNED_OCC
 #endif
-template <bool kLdsScene, bool kStats>
+template <bool kLdsScene, bool kStats, bool kBofs>
 __global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
-    step_body<MathPinned, kLdsScene, kStats>(a);
+    step_body<MathPinned, kLdsScene, kStats, kBofs>(a);
 }
 
 #ifdef RT_POOL_DEVICELIB_WAVES
@@ -87,10 +87,14 @@ namespace rtk {
 // Kernel variants: [schedule][math][scene in LDS][stats].
 
 template <class M, bool L, bool S>
-static KernelFn pick_sched(int sched) {
+static KernelFn pick_sched(int sched, bool bofs) {
     if (sched == kSchedStep) {
-        if (M::kId == MathDeviceLib::kId) return L ? kernel_entry_step_devicelib_lds<S> : kernel_entry_step_devicelib_global<S>;
-        return kernel_entry_step_pinned<L, S>;
+        if (M::kId == MathDeviceLib::kId) {
+            if (!L) return kernel_entry_step_devicelib_global<S>;
+            return bofs ? kernel_entry_step_devicelib_lds<S, true> : kernel_entry_step_devicelib_lds<S, false>;
+        }
+        if (!L) return kernel_entry_step_pinned<false, S, false>;
+        return bofs ? kernel_entry_step_pinned<true, S, true> : kernel_entry_step_pinned<true, S, false>;
     }
     if (sched == kSchedPool) {
         if (M::kId == MathDeviceLib::kId) return kernel_entry_pool_devicelib<L, S>;
@@ -99,19 +103,20 @@ static KernelFn pick_sched(int sched) {
     return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
 }
 
-static KernelFn pick(int sched, int math, bool lds, bool stats) {
-    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats);
+// bofs: LDS node records with the B planes at kOctB (KernelArgs::octB == kOctB)
+static KernelFn pick(int sched, int math, bool lds, bool stats, bool bofs) {
+    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats, bofs);
     if (math == MathDeviceLib::kId) {
-        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched) : pick_sched<MathDeviceLib, true, false>(sched);
-        return stats ? pick_sched<MathDeviceLib, false, true>(sched) : pick_sched<MathDeviceLib, false, false>(sched);
+        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched, bofs) : pick_sched<MathDeviceLib, true, false>(sched, bofs);
+        return stats ? pick_sched<MathDeviceLib, false, true>(sched, bofs) : pick_sched<MathDeviceLib, false, false>(sched, bofs);
     }
-    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched) : pick_sched<MathPinned, true, false>(sched);
-    return stats ? pick_sched<MathPinned, false, true>(sched) : pick_sched<MathPinned, false, false>(sched);
+    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched, bofs) : pick_sched<MathPinned, true, false>(sched, bofs);
+    return stats ? pick_sched<MathPinned, false, true>(sched, bofs) : pick_sched<MathPinned, false, false>(sched, bofs);
 }
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st) {
-    KernelFn fn = pick(sched, math, lds, stats);
+    KernelFn fn = pick(sched, math, lds, stats, lds && a.octB == kOctB);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), smem, st, a);
     return hipGetLastError();
 }
@@ -138,9 +143,9 @@ hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hip
     return hipGetLastError();
 }
 
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem) {
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem) {
     int blocks = 0;
-    KernelFn fn = pick(sched, math, lds, stats);
+    KernelFn fn = pick(sched, math, lds, stats, lds && bofs);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, smem) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }

@@ -21,6 +21,8 @@ struct KernelArgs {
     const float4* shadeMats;            // derived from slot 3: {diffuse, 1/(a+1)}, {specular, a^2/pi}, {emission, a^2-1}, {rough, a}
     uint32_t nNodes, nTris, nMats;
     uint32_t octStride;                 // LDS path: records per octant plane (nodes, END sentinel, odd pad)
+    uint32_t octB;                      // LDS path: float4 offset of the B planes (8 * octStride, or kOctB)
+    uint32_t octRecords;                // LDS path: float4s of node records (octB + 8 * octStride)
     uint32_t nTop;                      // global path: leading gNodes records staged in LDS
     uint32_t width, height;             // slots 4, 5
     uint32_t frameCount;                // slot 6 (slot 7, frameSeed, is unused by the reference)
@@ -72,11 +74,16 @@ constexpr uint32_t kRingWaveBytes = kRingSlots * 16u + kRingSlots * 4u;
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
 constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 
+// LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
+// the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address
+constexpr uint32_t kOctBMaxStride = 64;
+constexpr uint32_t kOctB = 8 * kOctBMaxStride;
+
 using KernelFn = void (*)(KernelArgs);
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, size_t smem);
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem);
 // accumulate the fused frames' radiances into the output (one pixel per lane)
 // (`key`: 4 words of per-kernel state for the sky shortcut, zeroed once; accum_key_body)
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st);
@@ -85,7 +92,7 @@ hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, 
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 // rt_kernels_shipped.hip: the MathShipped instantiations (own TU: OpenCL-default / and sqrt)
-KernelFn pick_shipped(int sched, bool lds, bool stats);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs);
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk

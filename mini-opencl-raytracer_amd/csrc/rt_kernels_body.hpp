@@ -53,6 +53,7 @@ constexpr float kInvPi = 0.31830988618f;    // kernel_bvh.cl:5
 constexpr float kMaxDist = 100000.0f;       // kernel_bvh.cl:7
 constexpr float kHitEps = 1.0e-8f;          // kernel_bvh.cl:101
 
+
 __device__ __forceinline__ F3 load3(const rt_float3& v) { return F3{v.x, v.y, v.z}; }
 
 // ---- RNG: kernel_bvh.cl:57-71 (integer, bit-exact by construction) ---------------------
@@ -134,10 +135,10 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     if (kLdsScene) {
         const int tid = threadIdx.x;
         float4* lo = smem;
-        float4* lt = lo + 16 * a.octStride;
+        float4* lt = lo + a.octRecords;
         float4* ls = lt + 3 * a.nTris;
         float4* lm = ls + 3 * a.nTris;
-        for (uint32_t i = tid; i < 16 * a.octStride; i += 256) lo[i] = a.octNodes[i];
+        for (uint32_t i = tid; i < a.octRecords; i += 256) lo[i] = a.octNodes[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
         for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
         for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
@@ -154,7 +155,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kLdsScene ? 16u * a.octStride + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
+    return kLdsScene ? a.octRecords + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -189,7 +190,7 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
                                            float t, uint32_t& next, uint32_t& first, uint32_t& count) {
     if (kOct) {
         const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
-        const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.octStride];
+        const float4 A = sc.onodes[i], B = sc.onodes[i + a.octB];
         float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
         float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
         t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
@@ -227,7 +228,7 @@ __device__ __forceinline__ bool node_visit(const SceneView& sc, const KernelArgs
 __device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
                                           float t, uint32_t& next, uint32_t& leaf_code) {
     const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
-    const float4 A = sc.onodes[i], B = sc.onodes[i + 8u * a.octStride];
+    const float4 A = sc.onodes[i], B = sc.onodes[i + a.octB];
     float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
     float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
     t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
@@ -240,6 +241,27 @@ __device__ __forceinline__ bool oct_visit(const SceneView& sc, const KernelArgs&
     next = (hit && !leaf) ? hn : mn;
     leaf_code = hn;
     return leaf;
+}
+
+// LDS walk with the walk word in `cur`: one node visit returning the next word --
+// the near child (< 2^24) or the leaf code on a passed box, else the skip pointer -- with the
+// skip pointer itself in `skip` (the continuation once a leaf's triangles are done).  One
+// compare and one select on the visit's own result: no mask arithmetic between them.
+template <bool kBofs>
+__device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                             float t, uint32_t& skip) {
+    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+    // kBofs (trees of <= kOctBMaxStride records per plane): the B record at a fixed offset, read
+    // with an immediate offset from A's address -- no second address on the dependent path
+    const float4 A = sc.onodes[i], B = sc.onodes[i + (kBofs ? kOctB : a.octB)];
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    skip = __float_as_uint(B.w);
+    return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
 }
 
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
@@ -276,9 +298,17 @@ template <class M, bool kUV = true>
 __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
                                              Traversal& h) {
     const TriEval e = tri_eval<M>(tri, r);
-    // (det < 1e-8 || -det > 1e-8) == det < 1e-8 (NaN falls through, as in the reference)
-    const bool ok = !(e.det < kHitEps) & !(e.u < 0.0f) & !(e.u > 1.0f) & !(e.v < 0.0f) &
-                    !(e.u + e.v > 1.0f) & (e.t < h.t);
+    // The reference's early returns (det < 1e-8, u < 0, u > 1, v < 0, u + v > 1; then t <
+    // isect.t) in VALU arithmetic rather than a chain of mask operations: for operands that are
+    // not NaN, x < y <=> x - y < 0 exactly (an IEEE difference of distinct floats is never
+    // rounded to zero or across it; denormals are kept), and minNum skips NaN operands, which
+    // the early returns let through as well ((det < 1e-8 || -det > 1e-8) == det < 1e-8).
+    // Rejected when any test fails; otherwise accepted iff t < isect.t.
+    const float rej = __builtin_fminf(__builtin_fminf(__builtin_fminf(e.det - kHitEps, e.u),
+                                                      __builtin_fminf(1.0f - e.u, e.v)),
+                                      1.0f - (e.u + e.v));
+    const float closer = rej < 0.0f ? -1.0f : h.t - e.t;
+    const bool ok = closer > 0.0f;
     if (ok) {
         h.t = e.t;
         h.prim = idx;
@@ -739,6 +769,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #define RT_TRI_BURST 2
 #endif
 
+
 // the same for scenes read from HBM/L2 (global path)
 #ifndef RT_GNODE_BURST
 #define RT_GNODE_BURST RT_NODE_BURST
@@ -750,7 +781,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
-template <class M, bool kLdsScene, bool kStats>
+template <class M, bool kLdsScene, bool kStats, bool kBofs = false>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
     // scenes read from HBM/L2: the render's waves issue ahead of co-resident accumulation waves
@@ -815,10 +846,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     Ray ray{};
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    uint32_t cur = 0;  // TRAV: node to visit; LEAF: node to continue at after the leaf
-    // LDS path: the walk word (see the node steps), kNotWalking outside TRAV; global path: the
-    // leaf's next triangle
-    uint32_t leaf_i = kLdsScene ? kNotWalking : 0u, leaf_end = 0;
+    // LDS path: `cur` is the walk word -- < 2^24 at node `cur`, count << 24 | first inside a
+    // passed leaf (the triangle steps count it down), kNotWalking outside TRAV -- and `leaf_i`
+    // the skip pointer a leaf continues at.  Global path: `cur` the node to visit or to continue
+    // at after the leaf, `leaf_i` the leaf's next triangle.
+    uint32_t cur = kLdsScene ? kNotWalking : 0u;
+    uint32_t leaf_i = 0u, leaf_end = 0;
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
@@ -941,7 +974,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         state = kTrav;
                         h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                         cur = 0;
-                        if (kLdsScene) leaf_i = 0u;  // walking, at the root
                         if (kStats) ++st.rays;
                     } else {
                         state = kDone;  // no bounce: radiance max(0, 0) = 0
@@ -1001,8 +1033,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                             cur = 0;
-                            if (kLdsScene) leaf_i = 0u;  // walking, at the root
-                            if (kStats) ++st.rays;
+                                if (kStats) ++st.rays;
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
                             if (a.hitIds && last_frame) {
@@ -1039,12 +1070,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (kLdsScene) {
                 // a walk parked on the END sentinel has finished the reference's traversal
                 // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
-                if (leaf_i < kLeafMin && cur == a.nNodes) {
+                if (cur == a.nNodes) {
                     state = kShade;
-                    leaf_i = kNotWalking;
+                    cur = kNotWalking;
                 }
-                n_trav = popc_ballot(leaf_i < kLeafMin);
-                n_leaf = popc_ballot((int32_t)leaf_i >= (int32_t)kLeafMin);
+                n_trav = popc_ballot(cur < kLeafMin);
+                n_leaf = popc_ballot((int32_t)cur >= (int32_t)kLeafMin);
             } else {
                 n_trav = popc_ballot(state == kTrav);
                 n_leaf = popc_ballot(state == kLeaf);
@@ -1071,15 +1102,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #pragma unroll
                 for (int rep = 0; rep < kNodeBurst; ++rep) {
                     if (kLdsScene) {
-                        // walk word (LDS path): < 2^24 = at node `cur`; a passed leaf stores its
-                        // code count << 24 | first, which the triangle steps count down; a walk
-                        // that reached END keeps visiting the sentinel (always missed, its own
-                        // successor) until the next decision -- no per-step end test
-                        if (leaf_i < kLeafMin) {
+                        // one node; a passed leaf leaves its code in `cur` (and the lane out of
+                        // the node steps), a walk at END keeps visiting the sentinel (always
+                        // missed, its own successor) until the next decision: no per-step
+                        // end test, one compare and one select per visit
+                        if (cur < kLeafMin) {
                             if (kStats && cur != a.nNodes) ++st.visits;
-                            uint32_t next, code;
-                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) leaf_i = code;
-                            cur = next;
+                            cur = oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
                         }
                     } else if (state == kTrav) {
                         if (kStats) ++st.visits;
@@ -1097,13 +1126,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #pragma unroll
                 for (int rep = 0; rep < kTriBurst; ++rep) {
                     if (kLdsScene) {
-                        // one triangle of the leaf; the last one drops the word below 2^24
-                        // (first + count), so the lane is back at node `cur` = the skip pointer
-                        if ((int32_t)leaf_i >= (int32_t)kLeafMin) {
+                        // one triangle of the leaf; after the last one the lane continues at
+                        // the leaf's skip pointer
+                        if ((int32_t)cur >= (int32_t)kLeafMin) {
                             if (kStats) ++st.tests;
-                            const uint32_t idx = leaf_i & 0x00ffffffu;
+                            const uint32_t idx = cur & 0x00ffffffu;
                             ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            leaf_i += 1u - kLeafMin;
+                            cur += 1u - kLeafMin;
+                            if (cur < kLeafMin) cur = leaf_i;
                         }
                     } else if (state == kLeaf) {
                         if (kStats) ++st.tests;
@@ -1140,11 +1170,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
                 state = kDone;
+                if (kLdsScene) cur = kNotWalking;
             } else {
                 state = kTrav;
                 h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                 cur = 0;
-                if (kLdsScene) leaf_i = 0u;  // walking, at the root
                 if (kStats) ++st.rays;
             }
         }

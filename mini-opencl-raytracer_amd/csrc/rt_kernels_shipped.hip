@@ -14,10 +14,10 @@ namespace rtk {
 
 // LDS-resident scenes run 5 waves per SIMD (VALU-bound); scenes read from HBM/L2 run 6 (load
 // latency to hide: bunny proxy -2.4 %, profiles/r01/global_path_waves_ab.txt)
-template <bool kStats>
+template <bool kStats, bool kBofs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
 void kernel_entry_step_shipped_lds(KernelArgs a) {
-    step_body<MathShipped, true, kStats>(a);
+    step_body<MathShipped, true, kStats, kBofs>(a);
 }
 template <bool kStats>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
@@ -36,15 +36,18 @@ __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4*
 }
 
 template <bool L, bool S>
-static KernelFn pick_sched_shipped(int sched) {
-    if (sched == kSchedStep) return L ? kernel_entry_step_shipped_lds<S> : kernel_entry_step_shipped_global<S>;
+static KernelFn pick_sched_shipped(int sched, bool bofs) {
+    if (sched == kSchedStep) {
+        if (!L) return kernel_entry_step_shipped_global<S>;
+        return bofs ? kernel_entry_step_shipped_lds<S, true> : kernel_entry_step_shipped_lds<S, false>;
+    }
     if (sched == kSchedPool) return kernel_entry_pool_shipped<L, S>;
     return sched == kSchedRegen ? kernel_entry_regen<MathShipped, L, S> : kernel_entry<MathShipped, L, S>;
 }
 
-KernelFn pick_shipped(int sched, bool lds, bool stats) {
-    if (lds) return stats ? pick_sched_shipped<true, true>(sched) : pick_sched_shipped<true, false>(sched);
-    return stats ? pick_sched_shipped<false, true>(sched) : pick_sched_shipped<false, false>(sched);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs) {
+    if (lds) return stats ? pick_sched_shipped<true, true>(sched, bofs) : pick_sched_shipped<true, false>(sched, bofs);
+    return stats ? pick_sched_shipped<false, true>(sched, bofs) : pick_sched_shipped<false, false>(sched, bofs);
 }
 
 __global__ __launch_bounds__(256) RT_ACCUM_OCC void accum_frames_shipped(KernelArgs a, const uint32_t* key) {
