@@ -75,7 +75,9 @@ def parse():
                    help="host: the reference's SAH build (default); device: rtBuildBVH linear BVH")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
-    p.add_argument("--sched", choices=["regen", "tiles", "step", "pool"], default="step")
+    p.add_argument("--sched", choices=["regen", "tiles", "step", "pool", "wavefront"], default="step",
+                   help="step (default): per-wave state machine in one persistent launch; wavefront: "
+                        "extend + shade launches per bounce over HBM ray queues (SURVEY 8(f.3))")
     p.add_argument("--launch", choices=["fused", "per-frame"], default="fused",
                    help="fused: the F frames of a step as one rtEnqueueKernelFrames call (one step launch "
                         "over (frame, pixel) work items + the per-pixel accumulation); per-frame: one "
@@ -151,7 +153,7 @@ def make_kernel(ctx, bufs, out, args):
     k.set_float3(N.CAMERA_UP, CAMERA[2])
     k.set_math_mode({"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[args.math])
     k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
-                    "pool": N.SCHED_POOL}[args.sched])
+                    "pool": N.SCHED_POOL, "wavefront": N.SCHED_WAVEFRONT}[args.sched])
     for t in args.tune:
         name, value = t.split("=", 1)
         k.set_tuning(name, int(value))
@@ -350,7 +352,7 @@ def main():
     value = rays_per_step * args.steps / elapsed / 1e6
     launches = max(1, ks["launches"])
     kernel_ms = ks["kernel_ms"] / launches
-    frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
+    frames_per_launch = args.frames if (args.launch == "fused" and args.sched in ("step", "wavefront")) else 1
     period_ms = ks["render_period_ms"] if frames_per_launch > 1 and not args.no_accum_overlap else 0.0
     rl = roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts, r.pixels)
     rl["accum_overlapped"] = frames_per_launch > 1 and not args.no_accum_overlap

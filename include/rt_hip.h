@@ -134,11 +134,19 @@ int rtKernelSetMathMode(rt_kernel k, int mode);
  *                             enough lanes are ready;
  * RT_SCHED_POOL            -- step traversal, plus a per-wave LDS pool of 64 path records:
  *                             lanes park finished traversals and keep tracing; shading runs
- *                             64 records at a time. */
+ *                             64 records at a time;
+ * RT_SCHED_WAVEFRONT       -- wavefront path tracing: per bounce an extend
+ *                             launch (traversal only, persistent waves pulling rays from an
+ *                             HBM ray queue) and a shade launch (one lane per queued path,
+ *                             continuations compacted into the next queue); radiance goes to
+ *                             per-frame slots and the fused accumulation launch, for
+ *                             rtEnqueueKernel too.  Queues take 72 B per work-item and frame.
+ *                             lightBounces outside 1..64 run the step schedule. */
 #define RT_SCHED_TILES 0
 #define RT_SCHED_REGEN 1
 #define RT_SCHED_STEP 2
 #define RT_SCHED_POOL 3
+#define RT_SCHED_WAVEFRONT 4
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
 /* Device-side BVH build (extension): a linear BVH (Morton codes, radix
@@ -247,7 +255,13 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   POOL_SHADE / PARK_MIN / LOW_WORK  pool schedule thresholds (64 / 16 / 32)
  *   TILE_MAJOR                        fused work order: -1 auto (default), 0 frame-major, 1 tile-major
  *   PERFRAME_SKY                      per-frame sky shortcut: 0 off, 1 large launches (default),
- *                                     2 always */
+ *                                     2 always
+ *   WF_REFILL_MIN                     wavefront extend: take queued rays once this many lanes
+ *                                     are free (1-64, default 8)
+ *   WF_STREAMS_PER_CU                 wavefront queues: streams per compute unit (0-64; default 0 =
+ *                                     the shade workgroups one CU holds at once)
+ *   WF_TOP_NODES                      wavefront extend, global path: top-of-tree nodes staged in
+ *                                     LDS (0-1024, default 256) */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -263,7 +277,10 @@ enum rt_tuning {
     RT_TUNE_PARK_MIN = 11,
     RT_TUNE_LOW_WORK = 12,
     RT_TUNE_TILE_MAJOR = 13,
-    RT_TUNE_PERFRAME_SKY = 14
+    RT_TUNE_PERFRAME_SKY = 14,
+    RT_TUNE_WF_REFILL_MIN = 15,
+    RT_TUNE_WF_STREAMS_PER_CU = 16,
+    RT_TUNE_WF_TOP_NODES = 17
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

@@ -63,6 +63,14 @@ struct rt_kernel_s {
     int pf_parity = 0;                 // per-frame key slot read by the next launch
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
+    // wavefront schedule: ray queues (two sets of 4 float4 planes), hit records, stream counts
+    uint32_t wf_refill_min = 8, wf_streams_per_cu = 0, wf_top_limit = 256;  // streams 0: auto
+    int wf_shade_occ[3][2] = {};       // [math][stats] -> shade workgroups per CU (0 = unknown)
+    float4* wf_q[2] = {};
+    float2* wf_hits = nullptr;
+    size_t wf_cap = 0;                 // entries per plane
+    uint32_t* wf_cnt = nullptr;        // 2 x (G + 1) words
+    size_t wf_cnt_cap = 0;             // words
     uint64_t range_first = 0, range_last = 0;
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
@@ -617,6 +625,10 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->render_done) (void)hipEventDestroy(k->render_done);
     if (k->first_end) (void)hipEventDestroy(k->first_end);
     for (hipEvent_t e : k->event_pool) (void)hipEventDestroy(e);
+    for (float4* q : k->wf_q)
+        if (q) (void)hipFree(q);
+    if (k->wf_hits) (void)hipFree(k->wf_hits);
+    if (k->wf_cnt) (void)hipFree(k->wf_cnt);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
     if (k->g_nodes) (void)hipFree(k->g_nodes);
@@ -657,7 +669,7 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
 
 int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames) {
     if (n_frames == 0) return RT_INVALID_VALUE;
-    if (n_frames == 1 || !k || k->sched != RT_SCHED_STEP) {
+    if (n_frames == 1 || !k || (k->sched != RT_SCHED_STEP && k->sched != RT_SCHED_WAVEFRONT)) {
         // one launch per frame (the other schedules have no fused form): same results
         if (!k) return RT_INVALID_KERNEL;
         uint32_t f0;
@@ -705,6 +717,15 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     if (rc) return rc;
     // a per-frame launch read-modify-writes the output: after the pending accumulations
     if (n_frames == 1) (void)qs(ctx);
+    // the schedule this launch runs: the wavefront one needs a bounded bounce loop (two launches
+    // per bounce), else the step schedule renders it (same bits)
+    int32_t lb;
+    std::memcpy(&lb, &k->u32[RT_ARG_LIGHT_BOUNCES], 4);
+    const bool wf = k->sched == RT_SCHED_WAVEFRONT && lb >= 1 && lb <= rtk::kWfMaxBounces;
+    const int si = wf ? rtk::kSchedWavefront : (k->sched == RT_SCHED_WAVEFRONT ? RT_SCHED_STEP : k->sched);
+    // radiance per (frame slot, work-item) + the accumulation launch: fused frames, and every
+    // wavefront render
+    const bool fused = n_frames > 1 || wf;
 
     uint64_t g0 = std::min<uint64_t>(k->range_first, global_work_size);
     uint64_t g1 = k->range_last ? std::min<uint64_t>(k->range_last, global_work_size) : global_work_size;
@@ -742,8 +763,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     const uint64_t row0 = g0 / W, row1 = (g1 + W - 1) / W;
     a.rowBegin = (uint32_t)row0;
     a.rowCount = (uint32_t)(row1 - row0);
-    const uint32_t tile = k->sched == RT_SCHED_TILES ? 16u : 8u;
-    if (k->band_period > 1 && k->sched == RT_SCHED_TILES) return RT_INVALID_OPERATION;
+    const uint32_t tile = si == RT_SCHED_TILES ? 16u : 8u;
+    if (k->band_period > 1 && si == RT_SCHED_TILES) return RT_INVALID_OPERATION;
     a.tilesX = (W + tile - 1) / tile;
     uint64_t tilesY = (row1 - row0 + tile - 1) / tile;
     a.bandPeriod = k->band_period;
@@ -769,7 +790,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.radStride = (uint32_t)g1;
     a.radBuf = nullptr;
     hipStream_t rstr = ctx->stream;  // the stream this launch's render goes to
-    if (n_frames > 1) {
+    if (fused) {
         // fused frames: radiance slots indexed by global work-item id (the lane packs
         // slot * g1 + gid into 32 bits); tiles x frames work items
         if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xffffffffull)
@@ -794,7 +815,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (me != hipSuccess) return map_hip(me);
             k->rad_buf_cap[rs] = need;
         }
-        if (ctx->overlap && !k->hit_ids) {
+        if (ctx->overlap && !k->hit_ids && !wf) {
             // the set's own render stream, after everything queued on the main stream so far
             // (buffer writes, per-frame launches) but not after the previous step's render or
             // accumulation: it fills the CUs that render's draining waves free.  (With hit
@@ -826,22 +847,29 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.refillMin = lds ? k->refill_min : k->refill_min_g;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g;
     a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
-    const size_t smem = (lds ? scene_bytes : (size_t)a.nTop * 64) + (k->sched == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
-                        (k->sched == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
-                        (k->sched == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
+    if (wf) a.nTop = std::min(a.nTop, k->wf_top_limit);
+    const size_t smem =
+        wf ? (lds ? ((size_t)a.octRecords + 3 * (size_t)k->n_tris) * 16 : (size_t)a.nTop * 64) +
+                 (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
+           : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
+                 (si == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
+                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math;
-    const int si = k->sched;
     const bool bofs = lds && a.octB == rtk::kOctB;
     int& occ = k->occ_cache[si][mi][lds][k->stats][bofs];
     if (occ == 0 || k->occ_smem[si][mi][lds][k->stats][bofs] != smem) {
-        occ = rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem);
+        occ = wf ? rtk::occupancy_wf_extend(k->math, lds, k->stats, bofs, smem)
+                 : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem);
         k->occ_smem[si][mi][lds][k->stats][bofs] = smem;
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
-    grid = std::min<uint64_t>(grid, k->sched == RT_SCHED_TILES ? n_tiles : (n_tiles * n_frames + 3) / 4);
+    // (wavefront extend: 8 waves per workgroup)
+    grid = std::min<uint64_t>(grid, si == RT_SCHED_TILES ? n_tiles
+                                    : wf                 ? (n_tiles * n_frames + 7) / 8
+                                                         : (n_tiles * n_frames + 3) / 4);
     if (grid == 0) grid = 1;
     {
         // bulk chunks only when every resident wave gets at least two of them; a small frame
@@ -858,12 +886,62 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch
     // start, which pays off from ~1k pixels per wave (4K) and not on small frames (512^2, 1080p)
-    if (n_frames == 1 && k->sched == RT_SCHED_STEP &&
+    if (n_frames == 1 && si == RT_SCHED_STEP &&
         (k->pf_sky == 2 || (k->pf_sky == 1 && g1 - g0 >= 1024u * 4u * grid))) {
         a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
         a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
     }
-    if (k->sched != RT_SCHED_TILES) {
+    rtk::WfArgs wa{};
+    float4* wq[2] = {};
+    uint32_t* wcnt[2] = {};
+    unsigned grid_s = 0;
+    if (wf) {
+        // queues for every (frame slot, work-item) of the launch, streams of 64-entry blocks
+        const uint64_t blocks = n_tiles * n_frames;
+        const size_t cap = (size_t)blocks * 64;
+        // streams: by default one per shade workgroup the GPU holds at once, so the shade
+        // launch is a single round of workgroups (no second, partly empty round)
+        int& occ_s = k->wf_shade_occ[mi][k->stats];
+        if (occ_s == 0) occ_s = rtk::occupancy_wf_shade(k->math, k->stats);
+        const uint64_t per_cu = k->wf_streams_per_cu ? k->wf_streams_per_cu : (uint64_t)occ_s;
+        const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)ctx->num_cus * per_cu));
+        if (k->wf_cap < cap) {
+            // earlier renders on this stream may still read them
+            hipError_t me = hipStreamSynchronize(rstr);
+            for (float4*& q : k->wf_q) {
+                if (q) (void)hipFree(q);
+                q = nullptr;
+            }
+            if (k->wf_hits) (void)hipFree(k->wf_hits);
+            k->wf_hits = nullptr;
+            k->wf_cap = 0;
+            for (float4*& q : k->wf_q)
+                if (me == hipSuccess) me = hipMalloc(&q, cap * 4 * sizeof(float4));
+            if (me == hipSuccess) me = hipMalloc(&k->wf_hits, cap * sizeof(float2));
+            if (me != hipSuccess) return map_hip(me);
+            k->wf_cap = cap;
+        }
+        if (k->wf_cnt_cap < 2 * ((size_t)G + 1)) {
+            hipError_t me = hipStreamSynchronize(rstr);
+            if (k->wf_cnt) (void)hipFree(k->wf_cnt);
+            k->wf_cnt = nullptr;
+            k->wf_cnt_cap = 0;
+            if (me == hipSuccess) me = hipMalloc(&k->wf_cnt, 2 * ((size_t)G + 1) * sizeof(uint32_t));
+            if (me != hipSuccess) return map_hip(me);
+            k->wf_cnt_cap = 2 * ((size_t)G + 1);
+        }
+        wq[0] = k->wf_q[0];
+        wq[1] = k->wf_q[1];
+        wcnt[0] = k->wf_cnt;
+        wcnt[1] = k->wf_cnt + G + 1;
+        wa.hits = k->wf_hits;
+        wa.cap = (uint32_t)cap;
+        wa.G = G;
+        wa.nBlocks = (uint32_t)blocks;
+        wa.refillMin = k->wf_refill_min;
+        grid_s = G;  // one workgroup per stream
+    }
+    if (si != RT_SCHED_TILES && !wf) {
         hipError_t me = hipMemsetAsync(a.workCounter, 0, 16, rstr);
         if (me != hipSuccess) return map_hip(me);
     }
@@ -874,14 +952,16 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if (!ev0 || !ev1) return RT_OUT_OF_RESOURCES;
         (void)hipEventRecord(ev0, rstr);
     }
-    hipError_t e = rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, rstr);
+    hipError_t e = wf ? rtk::launch_wavefront(a, wa, wq, wcnt, k->math, lds, k->stats, bofs, (unsigned)grid, smem,
+                                              grid_s, rstr)
+                      : rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, rstr);
     if (e != hipSuccess) return map_hip(e);
     if (k->timing) {
         (void)hipEventRecord(ev1, rstr);
         k->pending_events.emplace_back(ev0, ev1);
     }
     if (a.pfKeyIn) k->pf_parity ^= 1;
-    if (n_frames > 1) {
+    if (fused) {
         // fused frames: the gamma accumulation of every frame, in order, per pixel -- on the
         // accumulation stream after this render, overlapping whatever the main stream runs next
         // (the next fused render uses the other radiance set); qs() joins it back
@@ -998,7 +1078,8 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
 
 int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (!k) return RT_INVALID_KERNEL;
-    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP && sched != RT_SCHED_POOL)
+    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP && sched != RT_SCHED_POOL &&
+        sched != RT_SCHED_WAVEFRONT)
         return RT_INVALID_VALUE;
     k->sched = sched;
     return RT_SUCCESS;
@@ -1204,6 +1285,9 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_LOW_WORK: if (!in(1, 128)) return RT_INVALID_VALUE; k->low_work = (uint32_t)value; break;
         case RT_TUNE_TILE_MAJOR: if (!in(-1, 1)) return RT_INVALID_VALUE; k->tile_major = value; break;
         case RT_TUNE_PERFRAME_SKY: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_sky = value; break;
+        case RT_TUNE_WF_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->wf_refill_min = (uint32_t)value; break;
+        case RT_TUNE_WF_STREAMS_PER_CU: if (!in(0, 64)) return RT_INVALID_VALUE; k->wf_streams_per_cu = (uint32_t)value; break;
+        case RT_TUNE_WF_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->wf_top_limit = (uint32_t)value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1228,6 +1312,9 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_LOW_WORK: *value = (int)k->low_work; break;
         case RT_TUNE_TILE_MAJOR: *value = k->tile_major; break;
         case RT_TUNE_PERFRAME_SKY: *value = k->pf_sky; break;
+        case RT_TUNE_WF_REFILL_MIN: *value = (int)k->wf_refill_min; break;
+        case RT_TUNE_WF_STREAMS_PER_CU: *value = (int)k->wf_streams_per_cu; break;
+        case RT_TUNE_WF_TOP_NODES: *value = (int)k->wf_top_limit; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

@@ -150,6 +150,44 @@ int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs,
     return blocks > 0 ? blocks : 1;
 }
 
+// ---- wavefront schedule ------------------------------------------------------------------------
+static WfKernels pick_wf(int math, bool lds, bool stats, bool bofs) {
+    if (math == MathShipped::kId) return pick_wf_shipped(lds, stats, bofs);
+    if (math == MathDeviceLib::kId) return wf_pick<MathDeviceLib>(lds, stats, bofs);
+    return wf_pick<MathPinned>(lds, stats, bofs);
+}
+
+hipError_t launch_wavefront(const KernelArgs& a, WfArgs w, float4* const q[2], uint32_t* const cnt[2], int math,
+                            bool lds, bool stats, bool bofs, unsigned grid_e, size_t smem_e, unsigned grid_s,
+                            hipStream_t st) {
+    const WfKernels kf = pick_wf(math, lds, stats, bofs);
+    for (int b = 0; b < a.lightBounces; ++b) {
+        w.bounce = (uint32_t)b;
+        w.inQ = q[b & 1];
+        w.outQ = q[(b + 1) & 1];
+        w.inCnt = cnt[b & 1];
+        w.outCnt = cnt[(b + 1) & 1];
+        hipLaunchKernelGGL(kf.extend, dim3(grid_e), dim3(kWfExtendThreads), smem_e, st, a, w);
+        hipLaunchKernelGGL(kf.shade, dim3(grid_s), dim3(kWfShadeThreads), 0, st, a, w);
+    }
+    return hipGetLastError();
+}
+
+int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem) {
+    int blocks = 0;
+    const WfKernels kf = pick_wf(math, lds, stats, lds && bofs);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf.extend, kWfExtendThreads, smem) != hipSuccess)
+        return 1;
+    return blocks > 0 ? blocks : 1;
+}
+
+int occupancy_wf_shade(int math, bool stats) {
+    int blocks = 0;
+    const WfKernels kf = pick_wf(math, false, stats, false);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf.shade, kWfShadeThreads, 0) != hipSuccess) return 1;
+    return blocks > 0 ? blocks : 1;
+}
+
 hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
     if (n_tris) hipLaunchKernelGGL(pack_tris, dim3((n_tris + 255) / 256), dim3(256), 0, st, tris, pt, n_tris);

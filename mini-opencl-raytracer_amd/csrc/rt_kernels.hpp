@@ -59,7 +59,8 @@ constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounce
 constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
 constexpr int kSchedStep = 2;   // per-wave state machine: node / triangle steps, batched shading
 constexpr int kSchedPool = 3;   // step traversal + per-wave LDS path pool, full-wave shading
-constexpr int kNumSched = 4;
+constexpr int kSchedWavefront = 4;  // extend / shade launches per bounce over HBM ray queues
+constexpr int kNumSched = 5;
 // frames per fused launch (rtEnqueueKernelFrames splits longer runs)
 constexpr uint32_t kMaxFusedFrames = 8;
 // step schedule LDS per wave: the finish queue, 64 x {radiance, gid}
@@ -80,6 +81,39 @@ constexpr uint32_t kOctBMaxStride = 64;
 constexpr uint32_t kOctB = 8 * kOctBMaxStride;
 
 using KernelFn = void (*)(KernelArgs);
+
+// ---- wavefront schedule (rt_wavefront.hpp) ----------------------------------------------------
+// Per bounce b: extend(b) walks the BVH for every queued ray, shade(b) shades every queued path
+// and appends the continuations to the other queue.
+struct WfArgs {
+    const float4* inQ;        // bounce-b queue: 4 planes of `cap` float4:
+                              //   {o.xyz, path}, {d.xyz, seed}, {beta.xyz, -}, {radiance.xyz, -}
+    float4* outQ;             // bounce-(b+1) queue, same layout (written by shade)
+    float2* hits;             // [cap] {t, primitive bits}: extend(b) -> shade(b)
+    const uint32_t* inCnt;    // [G + 1]: entries per stream of inQ, [G] = their maximum
+    uint32_t* outCnt;         // [G + 1]: the same for outQ
+    uint32_t cap;             // entries per plane (nBlocks * 64)
+    uint32_t G;               // streams
+    uint32_t nBlocks;         // 64-entry blocks of the work-item space (nTiles * nFrames)
+    uint32_t bounce;          // this launch's bounce index
+    uint32_t refillMin;       // extend: take new rays once this many lanes are free
+};
+using WfKernelFn = void (*)(KernelArgs, WfArgs);
+struct WfKernels {
+    WfKernelFn extend, shade;
+};
+constexpr unsigned kWfExtendThreads = 512;  // extend workgroup: 8 waves (LDS scene staged once per 8)
+constexpr unsigned kWfShadeThreads = 256;   // shade workgroup: one stream, 256 paths per round
+constexpr int kWfMaxBounces = 64;            // longer bounce loops run the step schedule
+constexpr uint32_t kWfRingBytes = 64u * 32u;  // extend: per-wave ray ring ({o, position}, {d, -})
+// the launches of one wavefront render: for b < lightBounces, extend(b) then shade(b); queues and
+// counts alternate between q[0]/q[1] and cnt[0]/cnt[1]
+hipError_t launch_wavefront(const KernelArgs& a, WfArgs w, float4* const q[2], uint32_t* const cnt[2], int math,
+                            bool lds, bool stats, bool bofs, unsigned grid_e, size_t smem_e, unsigned grid_s,
+                            hipStream_t st);
+int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem);
+int occupancy_wf_shade(int math, bool stats);
+WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs);
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st);

@@ -1795,3 +1795,5 @@ __device__ __forceinline__ void material_record(const rt_cl_material& m, float4*
 }
 
 }  // namespace rtk
+
+#include "rt_wavefront.hpp"

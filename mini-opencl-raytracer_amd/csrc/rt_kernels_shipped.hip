@@ -64,6 +64,8 @@ hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipSt
     return hipGetLastError();
 }
 
+WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs) { return wf_pick<MathShipped>(lds, stats, bofs); }
+
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
     hipLaunchKernelGGL(pack_mats_shipped, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);
     return hipGetLastError();

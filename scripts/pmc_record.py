@@ -21,8 +21,9 @@ sys.path.insert(0, REPO)
 
 
 def render_kernel(names):
-    """The timed render launch: KernelEntry's step entry point without the stats variant."""
-    c = [k for k in names if "kernel_entry" in k and k.rstrip(")").endswith("false>(rtk::KernelArgs")]
+    """The timed render launch: KernelEntry's step entry point without the stats variant (its
+    first template argument, kStats, false)."""
+    c = [k for k in names if "kernel_entry" in k and "<false" in k]
     return c[0] if c else None
 
 
@@ -33,7 +34,7 @@ def main():
     sys.argv = ["bench.py"] + bench_args
     import bench
     args = bench.parse()
-    frames_per_launch = args.frames if (args.launch == "fused" and args.sched == "step") else 1
+    frames_per_launch = args.frames if (args.launch == "fused" and args.sched in ("step", "wavefront")) else 1
     key = bench.workload_key(args, int(os.environ.get("WORLD_SIZE", "1")), frames_per_launch)
 
     acc = defaultdict(lambda: defaultdict(list))
