@@ -247,7 +247,8 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   REFILL_MIN / SHADE_MIN            step schedule, LDS scenes: finish + refill when this many
  *                                     lanes are free (1-64, default 6); shade when this many are
  *                                     ready (1-64, default 44)
- *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (8 / 48)
+ *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (0-64; default 0 =
+ *                                     auto: 16 / 48 walking octant records, 8 / 48 the 64-B records)
  *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)
  *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64 (128 / 64)
  *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)
@@ -257,11 +258,15 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   PERFRAME_SKY                      per-frame sky shortcut: 0 off, 1 large launches (default),
  *                                     2 always
  *   WF_REFILL_MIN                     wavefront extend: take queued rays once this many lanes
- *                                     are free (1-64, default 8)
+ *                                     are free (1-64, default 32)
  *   WF_STREAMS_PER_CU                 wavefront queues: streams per compute unit (0-64; default 0 =
  *                                     the shade workgroups one CU holds at once)
  *   WF_TOP_NODES                      wavefront extend, global path: top-of-tree nodes staged in
- *                                     LDS (0-1024, default 256) */
+ *                                     LDS (0-1024, default 256)
+ *   GLOBAL_OCT                        step schedule, scenes not in LDS: 1 (default) = walk the
+ *                                     octant-resolved node records (32 B per node and octant) in
+ *                                     HBM/L2, 0 = the 64-B node records with the top of the tree
+ *                                     in LDS */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -280,7 +285,8 @@ enum rt_tuning {
     RT_TUNE_PERFRAME_SKY = 14,
     RT_TUNE_WF_REFILL_MIN = 15,
     RT_TUNE_WF_STREAMS_PER_CU = 16,
-    RT_TUNE_WF_TOP_NODES = 17
+    RT_TUNE_WF_TOP_NODES = 17,
+    RT_TUNE_GLOBAL_OCT = 18
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

@@ -34,6 +34,12 @@ constexpr uint64_t kKnownFlags =
     RT_MEM_READ_WRITE | RT_MEM_WRITE_ONLY | RT_MEM_READ_ONLY | RT_MEM_COPY_HOST_PTR;
 constexpr int kStatWords = 20;                // rt_stats counters kept on the device
 constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene path may use
+#ifndef RT_TIMELINE
+#define RT_TIMELINE 0
+#endif
+// diagnostic timeline builds (-DRT_TIMELINE=1, scripts/timeline.py) write a 64-bin histogram after
+// the primary hit ids: such a build requires hit buffers that long
+constexpr size_t kHitPad = RT_TIMELINE ? 64 : 0;
 
 }  // namespace
 
@@ -51,7 +57,9 @@ struct rt_kernel_s {
     // step schedule thresholds (lanes), swept on MI355X: LDS scenes (camera-ray ring)
     // profiles/r01/threshold_sweep_ring.txt; scenes read from HBM/L2 keep 8 / 48
     uint32_t refill_min = 6, shade_min = 44;
-    uint32_t refill_min_g = 8, shade_min_g = 48;
+    // scenes read from HBM/L2: 0 = auto (64-B node records 8 / 48; octant records 16 / 48,
+    // profiles/r02/goct_sweep.txt)
+    uint32_t refill_min_g = 0, shade_min_g = 0;
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
     uint32_t chunk_pixels = 128, tail_chunk = 64;  // pixels per work-counter fetch: bulk, tail
@@ -63,8 +71,11 @@ struct rt_kernel_s {
     int pf_parity = 0;                 // per-frame key slot read by the next launch
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
+    int global_oct = 1;                // scenes not in LDS: walk octant records in HBM/L2 (step;
+                                       // bunny proxy 1.80 -> 1.58 ms/frame, profiles/r02/goct_sweep.txt)
     // wavefront schedule: ray queues (two sets of 4 float4 planes), hit records, stream counts
-    uint32_t wf_refill_min = 8, wf_streams_per_cu = 0, wf_top_limit = 256;  // streams 0: auto
+    // (refill at 32 free lanes: bunny proxy 2.62 -> 2.45 ms/frame, profiles/r02/wavefront/sweep_bunny.txt)
+    uint32_t wf_refill_min = 32, wf_streams_per_cu = 0, wf_top_limit = 256;  // streams 0: auto
     int wf_shade_occ[3][2] = {};       // [math][stats] -> shade workgroups per CU (0 = unknown)
     float4* wf_q[2] = {};
     float2* wf_hits = nullptr;
@@ -711,7 +722,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     if (W == 0 || H == 0) return RT_INVALID_KERNEL_ARGS;
     rt_mem out = k->bufs[RT_ARG_BUFFER_OUT];
     if (out->size < global_work_size * 16) return RT_INVALID_GLOBAL_WORK_SIZE;
-    if (k->hit_ids && (k->hit_ids->size < global_work_size * 4 || k->hit_t->size < global_work_size * 4))
+    if (k->hit_ids && (k->hit_ids->size < (global_work_size + kHitPad) * 4 || k->hit_t->size < global_work_size * 4))
         return RT_INVALID_MEM_OBJECT;
     rc = prepare_scene(k);
     if (rc) return rc;
@@ -844,25 +855,30 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // (48 B per triangle, 64 B per material); no stack
     const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
-    a.refillMin = lds ? k->refill_min : k->refill_min_g;
-    a.shadeMin = lds ? k->shade_min : k->shade_min_g;
-    a.nTop = lds ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
+
+    // scenes too large for LDS: the step schedule may walk the octant records in HBM/L2
+    // (RT_TUNE_GLOBAL_OCT) instead of the 64-B global node records
+    const bool goct = !lds && (wf || si == RT_SCHED_STEP) && k->oct_ok && k->global_oct;
+    a.nTop = lds || goct ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
+    a.refillMin = lds ? k->refill_min : k->refill_min_g ? k->refill_min_g : goct ? 16u : 8u;
+    a.shadeMin = lds ? k->shade_min : k->shade_min_g ? k->shade_min_g : 48u;
     if (wf) a.nTop = std::min(a.nTop, k->wf_top_limit);
     const size_t smem =
         wf ? (lds ? ((size_t)a.octRecords + 3 * (size_t)k->n_tris) * 16 : (size_t)a.nTop * 64) +
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
                  (si == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
+                 (si == RT_SCHED_STEP && (lds || goct) && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math;
     const bool bofs = lds && a.octB == rtk::kOctB;
-    int& occ = k->occ_cache[si][mi][lds][k->stats][bofs];
-    if (occ == 0 || k->occ_smem[si][mi][lds][k->stats][bofs] != smem) {
-        occ = wf ? rtk::occupancy_wf_extend(k->math, lds, k->stats, bofs, smem)
-                 : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem);
-        k->occ_smem[si][mi][lds][k->stats][bofs] = smem;
+    const int var = bofs || goct;  // occupancy cache: the variant slot
+    int& occ = k->occ_cache[si][mi][lds][k->stats][var];
+    if (occ == 0 || k->occ_smem[si][mi][lds][k->stats][var] != smem) {
+        occ = wf ? rtk::occupancy_wf_extend(k->math, lds, k->stats, bofs, smem, goct)
+                 : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct);
+        k->occ_smem[si][mi][lds][k->stats][var] = smem;
     }
     uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
@@ -953,8 +969,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         (void)hipEventRecord(ev0, rstr);
     }
     hipError_t e = wf ? rtk::launch_wavefront(a, wa, wq, wcnt, k->math, lds, k->stats, bofs, (unsigned)grid, smem,
-                                              grid_s, rstr)
-                      : rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, rstr);
+                                              grid_s, rstr, goct)
+                      : rtk::launch_kernel_entry(a, si, k->math, lds, k->stats, (unsigned)grid, smem, rstr, goct);
     if (e != hipSuccess) return map_hip(e);
     if (k->timing) {
         (void)hipEventRecord(ev1, rstr);
@@ -1266,8 +1282,8 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
     switch (param) {
         case RT_TUNE_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min = (uint32_t)value; break;
         case RT_TUNE_SHADE_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->shade_min = (uint32_t)value; break;
-        case RT_TUNE_REFILL_MIN_GLOBAL: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min_g = (uint32_t)value; break;
-        case RT_TUNE_SHADE_MIN_GLOBAL: if (!in(1, 64)) return RT_INVALID_VALUE; k->shade_min_g = (uint32_t)value; break;
+        case RT_TUNE_REFILL_MIN_GLOBAL: if (!in(0, 64)) return RT_INVALID_VALUE; k->refill_min_g = (uint32_t)value; break;
+        case RT_TUNE_SHADE_MIN_GLOBAL: if (!in(0, 64)) return RT_INVALID_VALUE; k->shade_min_g = (uint32_t)value; break;
         case RT_TUNE_STEP_WEIGHT_NODE: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_node = (uint32_t)value; break;
         case RT_TUNE_STEP_WEIGHT_LEAF: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_leaf = (uint32_t)value; break;
         case RT_TUNE_CHUNK_PIXELS:
@@ -1288,6 +1304,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_WF_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->wf_refill_min = (uint32_t)value; break;
         case RT_TUNE_WF_STREAMS_PER_CU: if (!in(0, 64)) return RT_INVALID_VALUE; k->wf_streams_per_cu = (uint32_t)value; break;
         case RT_TUNE_WF_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->wf_top_limit = (uint32_t)value; break;
+        case RT_TUNE_GLOBAL_OCT: if (!in(0, 1)) return RT_INVALID_VALUE; k->global_oct = value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1315,6 +1332,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_WF_REFILL_MIN: *value = (int)k->wf_refill_min; break;
         case RT_TUNE_WF_STREAMS_PER_CU: *value = (int)k->wf_streams_per_cu; break;
         case RT_TUNE_WF_TOP_NODES: *value = (int)k->wf_top_limit; break;
+        case RT_TUNE_GLOBAL_OCT: *value = k->global_oct; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

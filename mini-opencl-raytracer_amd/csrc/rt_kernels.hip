@@ -21,14 +21,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLO
 void kernel_entry_step_devicelib_global(KernelArgs a) {
     step_body<MathDeviceLib, false, kStats>(a);
 }
+template <bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOCT_WAVES, 8)))
+void kernel_entry_step_devicelib_goct(KernelArgs a) {
+    step_body<MathDeviceLib, true, kStats, false, true>(a);
+}
 #ifdef RT_STEP_PINNED_WAVES
 #define RT_STEP_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
 #else
 #define RT_STEP_PINNED_OCC
 #endif
-template <bool kLdsScene, bool kStats, bool kBofs>
+template <bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct = false>
 __global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
-    step_body<MathPinned, kLdsScene, kStats, kBofs>(a);
+    step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct>(a);
 }
 
 #ifdef RT_POOL_DEVICELIB_WAVES
@@ -87,13 +92,13 @@ namespace rtk {
 // Kernel variants: [schedule][math][scene in LDS][stats].
 
 template <class M, bool L, bool S>
-static KernelFn pick_sched(int sched, bool bofs) {
+static KernelFn pick_sched(int sched, bool bofs, bool goct) {
     if (sched == kSchedStep) {
         if (M::kId == MathDeviceLib::kId) {
-            if (!L) return kernel_entry_step_devicelib_global<S>;
+            if (!L) return goct ? kernel_entry_step_devicelib_goct<S> : kernel_entry_step_devicelib_global<S>;
             return bofs ? kernel_entry_step_devicelib_lds<S, true> : kernel_entry_step_devicelib_lds<S, false>;
         }
-        if (!L) return kernel_entry_step_pinned<false, S, false>;
+        if (!L) return goct ? kernel_entry_step_pinned<true, S, false, true> : kernel_entry_step_pinned<false, S, false>;
         return bofs ? kernel_entry_step_pinned<true, S, true> : kernel_entry_step_pinned<true, S, false>;
     }
     if (sched == kSchedPool) {
@@ -103,20 +108,21 @@ static KernelFn pick_sched(int sched, bool bofs) {
     return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
 }
 
-// bofs: LDS node records with the B planes at kOctB (KernelArgs::octB == kOctB)
-static KernelFn pick(int sched, int math, bool lds, bool stats, bool bofs) {
-    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats, bofs);
+// bofs: LDS node records with the B planes at kOctB (KernelArgs::octB == kOctB); goct: a scene
+// too large for LDS walked through its octant records in HBM/L2 (step schedule)
+static KernelFn pick(int sched, int math, bool lds, bool stats, bool bofs, bool goct) {
+    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats, bofs, goct);
     if (math == MathDeviceLib::kId) {
-        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched, bofs) : pick_sched<MathDeviceLib, true, false>(sched, bofs);
-        return stats ? pick_sched<MathDeviceLib, false, true>(sched, bofs) : pick_sched<MathDeviceLib, false, false>(sched, bofs);
+        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched, bofs, false) : pick_sched<MathDeviceLib, true, false>(sched, bofs, false);
+        return stats ? pick_sched<MathDeviceLib, false, true>(sched, bofs, goct) : pick_sched<MathDeviceLib, false, false>(sched, bofs, goct);
     }
-    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched, bofs) : pick_sched<MathPinned, true, false>(sched, bofs);
-    return stats ? pick_sched<MathPinned, false, true>(sched, bofs) : pick_sched<MathPinned, false, false>(sched, bofs);
+    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched, bofs, false) : pick_sched<MathPinned, true, false>(sched, bofs, false);
+    return stats ? pick_sched<MathPinned, false, true>(sched, bofs, goct) : pick_sched<MathPinned, false, false>(sched, bofs, goct);
 }
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
-                               size_t smem, hipStream_t st) {
-    KernelFn fn = pick(sched, math, lds, stats, lds && a.octB == kOctB);
+                               size_t smem, hipStream_t st, bool goct) {
+    KernelFn fn = pick(sched, math, lds, stats, lds && a.octB == kOctB, goct);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), smem, st, a);
     return hipGetLastError();
 }
@@ -143,24 +149,24 @@ hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hip
     return hipGetLastError();
 }
 
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem) {
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct) {
     int blocks = 0;
-    KernelFn fn = pick(sched, math, lds, stats, lds && bofs);
+    KernelFn fn = pick(sched, math, lds, stats, lds && bofs, goct);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, smem) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }
 
 // ---- wavefront schedule ------------------------------------------------------------------------
-static WfKernels pick_wf(int math, bool lds, bool stats, bool bofs) {
-    if (math == MathShipped::kId) return pick_wf_shipped(lds, stats, bofs);
-    if (math == MathDeviceLib::kId) return wf_pick<MathDeviceLib>(lds, stats, bofs);
-    return wf_pick<MathPinned>(lds, stats, bofs);
+static WfKernels pick_wf(int math, bool lds, bool stats, bool bofs, bool goct) {
+    if (math == MathShipped::kId) return pick_wf_shipped(lds, stats, bofs, goct);
+    if (math == MathDeviceLib::kId) return wf_pick<MathDeviceLib>(lds, stats, bofs, goct);
+    return wf_pick<MathPinned>(lds, stats, bofs, goct);
 }
 
 hipError_t launch_wavefront(const KernelArgs& a, WfArgs w, float4* const q[2], uint32_t* const cnt[2], int math,
                             bool lds, bool stats, bool bofs, unsigned grid_e, size_t smem_e, unsigned grid_s,
-                            hipStream_t st) {
-    const WfKernels kf = pick_wf(math, lds, stats, bofs);
+                            hipStream_t st, bool goct) {
+    const WfKernels kf = pick_wf(math, lds, stats, bofs, goct);
     for (int b = 0; b < a.lightBounces; ++b) {
         w.bounce = (uint32_t)b;
         w.inQ = q[b & 1];
@@ -173,9 +179,9 @@ hipError_t launch_wavefront(const KernelArgs& a, WfArgs w, float4* const q[2], u
     return hipGetLastError();
 }
 
-int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem) {
+int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem, bool goct) {
     int blocks = 0;
-    const WfKernels kf = pick_wf(math, lds, stats, lds && bofs);
+    const WfKernels kf = pick_wf(math, lds, stats, lds && bofs, goct);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf.extend, kWfExtendThreads, smem) != hipSuccess)
         return 1;
     return blocks > 0 ? blocks : 1;
@@ -183,7 +189,7 @@ int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem) 
 
 int occupancy_wf_shade(int math, bool stats) {
     int blocks = 0;
-    const WfKernels kf = pick_wf(math, false, stats, false);
+    const WfKernels kf = pick_wf(math, false, stats, false, false);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf.shade, kWfShadeThreads, 0) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }

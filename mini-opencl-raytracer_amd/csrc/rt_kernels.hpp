@@ -110,14 +110,16 @@ constexpr uint32_t kWfRingBytes = 64u * 32u;  // extend: per-wave ray ring ({o, 
 // counts alternate between q[0]/q[1] and cnt[0]/cnt[1]
 hipError_t launch_wavefront(const KernelArgs& a, WfArgs w, float4* const q[2], uint32_t* const cnt[2], int math,
                             bool lds, bool stats, bool bofs, unsigned grid_e, size_t smem_e, unsigned grid_s,
-                            hipStream_t st);
-int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem);
+                            hipStream_t st, bool goct);
+int occupancy_wf_extend(int math, bool lds, bool stats, bool bofs, size_t smem, bool goct);
 int occupancy_wf_shade(int math, bool stats);
-WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs);
+WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs, bool goct);
 
+// goct (step schedule, scene not in LDS): walk the octant records in HBM/L2 instead of the
+// 64-B global node records
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
-                               size_t smem, hipStream_t st);
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem);
+                               size_t smem, hipStream_t st, bool goct = false);
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct = false);
 // accumulate the fused frames' radiances into the output (one pixel per lane)
 // (`key`: 4 words of per-kernel state for the sky shortcut, zeroed once; accum_key_body)
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st);
@@ -126,7 +128,7 @@ hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, 
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 // rt_kernels_shipped.hip: the MathShipped instantiations (own TU: OpenCL-default / and sqrt)
-KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct);
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk

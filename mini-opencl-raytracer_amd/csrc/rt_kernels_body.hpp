@@ -45,6 +45,9 @@
 #ifndef RT_STEP_GLOBAL_WAVES
 #define RT_STEP_GLOBAL_WAVES 6  // the same entry points for scenes read from HBM/L2
 #endif
+#ifndef RT_STEP_GOCT_WAVES
+#define RT_STEP_GOCT_WAVES 5  // ... walking their octant records (5: no spills; 6 spills 23 VGPRs)
+#endif
 
 namespace rtk {
 
@@ -128,10 +131,13 @@ constexpr uint32_t kEnd = 0xffffffffu;  // "stack empty": traversal finished (gl
 // every ray misses and whose successors are itself (rt_capi.cpp, build_oct_nodes).
 constexpr uint32_t kLeafMin = 1u << 24;
 
-// Scene into LDS once per workgroup (when it fits), else read in place.
-template <bool kLdsScene>
+// Scene into LDS once per workgroup (when it fits), else read in place.  kGlobalOct: the octant
+// records, triangles and shading records of a scene too large for LDS, read from HBM/L2 by the
+// LDS path's walk (same record formats, nothing staged).
+template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    if (kGlobalOct) return SceneView{nullptr, a.packedTris, a.octNodes, a.shadeTris, a.shadeMats};
     if (kLdsScene) {
         const int tid = threadIdx.x;
         float4* lo = smem;
@@ -153,9 +159,9 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 }
 
 // LDS float4s of the scene (the finish queue / pool follow it)
-template <bool kLdsScene>
+template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kLdsScene ? a.octRecords + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
+    return kGlobalOct ? 0u : kLdsScene ? a.octRecords + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -781,14 +787,14 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
-template <class M, bool kLdsScene, bool kStats, bool kBofs = false>
+template <class M, bool kLdsScene, bool kStats, bool kBofs = false, bool kGlobalOct = false>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
     // scenes read from HBM/L2: the render's waves issue ahead of co-resident accumulation waves
     // (second stream), which then only fill the slots the render leaves idle (bunny proxy -1.5 %;
     // profiles/r01/render_priority_ab.txt); traversal steps raise it further (below)
     if (!kLdsScene) __builtin_amdgcn_s_setprio(1);
-    const SceneView sc = stage_scene<kLdsScene>(a);
+    const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
@@ -822,14 +828,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 
     // per-wave finish queue in LDS (after the scene): {radiance, gid} of finished paths
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    float4* fq = smem + lds_scene_f4<kLdsScene>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
+    float4* fq = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
     uint32_t fq_n = 0;  // wave-uniform
 #if RT_RAY_RING
     // LDS scenes: per-wave ring of camera rays, generated one whole 8x8 tile (64 lanes) at a
     // time and handed to idle lanes at refill -- create_ray then runs on full waves instead of
     // on the few lanes a refill serves.  Same rays, same seeds, same pixel order.
     constexpr bool kRing = kLdsScene;
-    float4* ring_d = smem + lds_scene_f4<kLdsScene>(a) + (fused ? 0u : 4u * kFinishSlots) +
+    float4* ring_d = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
                      (uint32_t)(tid >> 6) * (kRingWaveBytes / 16u);
     uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + kRingSlots);
 #else

@@ -24,6 +24,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLO
 void kernel_entry_step_shipped_global(KernelArgs a) {
     step_body<MathShipped, false, kStats>(a);
 }
+// octant records read from HBM/L2 (scenes too large for LDS): the LDS path's walk
+template <bool kStats>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOCT_WAVES, 8)))
+void kernel_entry_step_shipped_goct(KernelArgs a) {
+    step_body<MathShipped, true, kStats, false, true>(a);
+}
 template <bool kLdsScene, bool kStats>
 __global__ __launch_bounds__(256) void kernel_entry_pool_shipped(KernelArgs a) {
     pool_body<MathShipped, kLdsScene, kStats>(a);
@@ -36,18 +42,18 @@ __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4*
 }
 
 template <bool L, bool S>
-static KernelFn pick_sched_shipped(int sched, bool bofs) {
+static KernelFn pick_sched_shipped(int sched, bool bofs, bool goct) {
     if (sched == kSchedStep) {
-        if (!L) return kernel_entry_step_shipped_global<S>;
+        if (!L) return goct ? kernel_entry_step_shipped_goct<S> : kernel_entry_step_shipped_global<S>;
         return bofs ? kernel_entry_step_shipped_lds<S, true> : kernel_entry_step_shipped_lds<S, false>;
     }
     if (sched == kSchedPool) return kernel_entry_pool_shipped<L, S>;
     return sched == kSchedRegen ? kernel_entry_regen<MathShipped, L, S> : kernel_entry<MathShipped, L, S>;
 }
 
-KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs) {
-    if (lds) return stats ? pick_sched_shipped<true, true>(sched, bofs) : pick_sched_shipped<true, false>(sched, bofs);
-    return stats ? pick_sched_shipped<false, true>(sched, bofs) : pick_sched_shipped<false, false>(sched, bofs);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct) {
+    if (lds) return stats ? pick_sched_shipped<true, true>(sched, bofs, false) : pick_sched_shipped<true, false>(sched, bofs, false);
+    return stats ? pick_sched_shipped<false, true>(sched, bofs, goct) : pick_sched_shipped<false, false>(sched, bofs, goct);
 }
 
 __global__ __launch_bounds__(256) RT_ACCUM_OCC void accum_frames_shipped(KernelArgs a, const uint32_t* key) {
@@ -64,7 +70,9 @@ hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipSt
     return hipGetLastError();
 }
 
-WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs) { return wf_pick<MathShipped>(lds, stats, bofs); }
+WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs, bool goct) {
+    return wf_pick<MathShipped>(lds, stats, bofs, goct);
+}
 
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st) {
     hipLaunchKernelGGL(pack_mats_shipped, dim3((n_mats + 255) / 256), dim3(256), 0, st, mats, pm, n_mats);

@@ -69,13 +69,17 @@ __device__ __forceinline__ uint32_t wf_pos(uint32_t v, uint32_t k, uint32_t G) {
 // entries, or one 8x8 tile of camera rays) at a time; free lanes take rays from it.
 constexpr uint32_t kWfRingF4 = kWfRingBytes / 16u;  // float4 per wave
 
-template <class M, bool kLdsScene, bool kStats, bool kBofs>
+template <class M, bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct = false>
 __device__ __forceinline__ void wf_extend_body(const KernelArgs& a, const WfArgs& w) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     SceneView sc;
     uint32_t scene_f4;
-    if (kLdsScene) {
+    if (kGlobalOct) {
+        // octant records and triangles of a scene too large for LDS, read from HBM/L2
+        sc = SceneView{nullptr, a.packedTris, a.octNodes, nullptr, nullptr};
+        scene_f4 = 0;
+    } else if (kLdsScene) {
         float4* lo = smem;
         float4* lt = lo + a.octRecords;
         for (uint32_t i = tid; i < a.octRecords; i += nthr) lo[i] = a.octNodes[i];
@@ -357,10 +361,10 @@ __device__ __forceinline__ void wf_shade_body(const KernelArgs& a, const WfArgs&
 #ifndef RT_WF_EXTEND_WAVES
 #define RT_WF_EXTEND_WAVES 8
 #endif
-template <class M, bool kLdsScene, bool kStats, bool kBofs>
+template <class M, bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct = false>
 __global__ __launch_bounds__(kWfExtendThreads) __attribute__((amdgpu_waves_per_eu(RT_WF_EXTEND_WAVES, 8)))
 void wf_extend(KernelArgs a, WfArgs w) {
-    wf_extend_body<M, kLdsScene, kStats, kBofs>(a, w);
+    wf_extend_body<M, kLdsScene, kStats, kBofs, kGlobalOct>(a, w);
 }
 template <class M, bool kStats>
 __global__ __launch_bounds__(kWfShadeThreads) void wf_shade(KernelArgs a, WfArgs w) {
@@ -368,13 +372,15 @@ __global__ __launch_bounds__(kWfShadeThreads) void wf_shade(KernelArgs a, WfArgs
 }
 
 template <class M, bool S>
-WfKernels wf_pick_s(bool lds, bool bofs) {
-    WfKernelFn e = lds ? (bofs ? wf_extend<M, true, S, true> : wf_extend<M, true, S, false>) : wf_extend<M, false, S, false>;
+WfKernels wf_pick_s(bool lds, bool bofs, bool goct) {
+    WfKernelFn e = lds    ? (bofs ? wf_extend<M, true, S, true> : wf_extend<M, true, S, false>)
+                   : goct ? wf_extend<M, true, S, false, true>
+                          : wf_extend<M, false, S, false>;
     return WfKernels{e, wf_shade<M, S>};
 }
 template <class M>
-WfKernels wf_pick(bool lds, bool stats, bool bofs) {
-    return stats ? wf_pick_s<M, true>(lds, bofs) : wf_pick_s<M, false>(lds, bofs);
+WfKernels wf_pick(bool lds, bool stats, bool bofs, bool goct) {
+    return stats ? wf_pick_s<M, true>(lds, bofs, goct) : wf_pick_s<M, false>(lds, bofs, goct);
 }
 
 }  // namespace rtk

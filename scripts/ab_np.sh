@@ -1,0 +1,7 @@
+set -u
+mkdir -p gpurun_out
+bash scripts/ab_quick.sh 3 || exit 1
+for v in np tp; do
+  RT_HIP_LIB=mini-opencl-raytracer_amd/lib/variants/librt_hip_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_fused_frames.py tests/test_benched_path.py tests/test_ref_opencl.py -x -q --timeout 200 --timeout-method thread > gpurun_out/np_tests_$v.log 2>&1
+  echo "$v tests rc=$?"; tail -2 gpurun_out/np_tests_$v.log
+done

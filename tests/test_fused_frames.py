@@ -206,3 +206,25 @@ def test_readback_on_accum_stream_after_per_frame_launches(cornell, frames):
     dst.release()
     r.close()
     assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_DEVICELIB, N.MATH_SHIPPED])
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("goct", [0, 1])
+def test_global_scene_walks(cornell, math, fused, goct):
+    """Scenes not in LDS: the octant-resolved records read from HBM/L2 (RT_TUNE_GLOBAL_OCT 1, the
+    default) or the 64-B global node records with the top of the tree in LDS (0) -- the same
+    visits in the same order as the LDS walk: same bits."""
+    W, H = 256, 144
+    _same(_render(cornell, W, H, 1, 5, fused, math, force_global=True, tuning={"global_oct": goct}),
+          _render(cornell, W, H, 1, 5, False, math))
+
+
+@pytest.mark.parametrize("sched", [N.SCHED_STEP, N.SCHED_WAVEFRONT])
+def test_global_scene_walks_bunny_proxy(sched):
+    from clrt import proxy
+    sc = proxy.bunny_proxy()
+    W, H = 320, 180
+    want = _render(sc, W, H, 1, 4, False, tuning={"global_oct": 0})
+    for goct in (0, 1):
+        _same(_render(sc, W, H, 1, 4, True, sched=sched, tuning={"global_oct": goct}), want)

@@ -103,7 +103,8 @@ def test_wavefront_odd_sizes(cornell, W, H):
 
 @pytest.mark.parametrize("tuning", [{"wf_streams_per_cu": 1}, {"wf_streams_per_cu": 64},
                                     {"wf_refill_min": 1}, {"wf_refill_min": 64},
-                                    {"wf_top_nodes": 0, "tile_major": 1}, {"wf_top_nodes": 1024}])
+                                    {"wf_top_nodes": 0, "tile_major": 1, "global_oct": 0},
+                                    {"wf_top_nodes": 1024, "global_oct": 0}])
 def test_wavefront_tuning_keeps_bits(cornell, tuning):
     W, H = 224, 128
     for fg in (False, True):
