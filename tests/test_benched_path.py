@@ -32,9 +32,9 @@ def _open_ref(variant):
         pytest.skip(f"no OpenCL GPU device for the reference: {e}")
 
 
-def _bench_steps(scene, steps=3, frames=8):
+def _bench_steps(scene, steps=3, frames=8, sched=N.SCHED_STEP):
     """bench.py's timed loop on one GPU: `steps` fused 8-frame renders queued back to back."""
-    r = HipRenderer(scene, W4K, H4K, math=N.MATH_SHIPPED, hits=True)
+    r = HipRenderer(scene, W4K, H4K, math=N.MATH_SHIPPED, hits=True, sched=sched)
     for _ in range(steps):
         r.frame(1, light_bounces=9, n_frames=frames)
     r.ctx.Finish()
@@ -45,12 +45,12 @@ def _bench_steps(scene, steps=3, frames=8):
     return got, ids, t, in_lds
 
 
-def _check(scene, want_lds, frames):
+def _check(scene, want_lds, frames, sched=N.SCHED_STEP):
     ref = _open_ref("shipped")
     want = ref.render(scene, W4K, H4K, frames=range(1, frames + 1), light_bounces=9)[:, :3]
     ids_r, t_r = ref.primary_hits(scene, W4K, H4K, frame=frames)
     ref.close()
-    got, ids, t, in_lds = _bench_steps(scene, frames=frames)
+    got, ids, t, in_lds = _bench_steps(scene, frames=frames, sched=sched)
     assert in_lds == want_lds
     nd = bits_differ(got, want)
     assert nd == 0, f"{nd} radiance words differ, max rel {rel_err(got, want).max():.3g}"
@@ -65,3 +65,14 @@ def test_benched_cornell_4k_8spp_equals_live_reference(cornell):
 def test_benched_bunny_4k_8spp_equals_live_reference():
     import clrt.proxy as P
     _check(P.bunny_proxy(), False, 8)
+
+
+@pytest.mark.parametrize("scene_name", ["cornell", "bunny"])
+def test_wavefront_4k_8spp_equals_live_reference(cornell, scene_name):
+    """bench.py --sched wavefront (extend / shade launches per bounce over the HBM ray queues)
+    at full size: the same bits as the reference."""
+    if scene_name == "cornell":
+        _check(cornell, True, 8, sched=N.SCHED_WAVEFRONT)
+    else:
+        import clrt.proxy as P
+        _check(P.bunny_proxy(), False, 8, sched=N.SCHED_WAVEFRONT)
