@@ -834,7 +834,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // LDS scenes: per-wave ring of camera rays, generated one whole 8x8 tile (64 lanes) at a
     // time and handed to idle lanes at refill -- create_ray then runs on full waves instead of
     // on the few lanes a refill serves.  Same rays, same seeds, same pixel order.
-    constexpr bool kRing = kLdsScene;
+    // (not for the octant walk over HBM/L2: bunny proxy 1.572 -> 1.536 ms/frame without it,
+    // profiles/r02/goct/ring_ab_bunny.txt)
+    constexpr bool kRing = kLdsScene && !kGlobalOct;
     float4* ring_d = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
                      (uint32_t)(tid >> 6) * (kRingWaveBytes / 16u);
     uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + kRingSlots);
