@@ -783,6 +783,14 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_GTRI_BURST
 #define RT_GTRI_BURST RT_TRI_BURST
 #endif
+// ... and for the octant walk over HBM/L2 (node bursts of 3-5 tie, 6 is 1.7 % slower, 2 and 8
+// 1-2 %: profiles/r02/goct/burst_ab_bunny.txt)
+#ifndef RT_ONODE_BURST
+#define RT_ONODE_BURST 4
+#endif
+#ifndef RT_OTRI_BURST
+#define RT_OTRI_BURST RT_TRI_BURST
+#endif
 
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
@@ -1104,8 +1112,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     u_nlanes += n_trav;
                 }
             }
-            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
-            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
+            constexpr int kNodeBurst = kGlobalOct ? RT_ONODE_BURST : kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
+            constexpr int kTriBurst = kGlobalOct ? RT_OTRI_BURST : kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
             if (!leaf_step) {
 #pragma unroll
                 for (int rep = 0; rep < kNodeBurst; ++rep) {
