@@ -97,11 +97,11 @@ struct rt_kernel_s {
     uint64_t period_intervals = 0;
     // fused frames: radiance and primary-miss flag per (frame slot, work-item), two sets used
     // alternately so a render can run while the previous launch's accumulation reads the other
-    float4* rad_buf[2] = {};
-    uint8_t* frame_flags[2] = {};
-    size_t rad_buf_cap[2] = {};        // float4 slots
-    hipEvent_t rad_free[2] = {};       // recorded on astream after the accumulation reading the set
-    bool rad_busy[2] = {};
+    float4* rad_buf[RT_RAD_SETS] = {};
+    uint8_t* frame_flags[RT_RAD_SETS] = {};
+    size_t rad_buf_cap[RT_RAD_SETS] = {};  // float4 slots
+    hipEvent_t rad_free[RT_RAD_SETS] = {};  // recorded on astream after the accumulation reading the set
+    bool rad_busy[RT_RAD_SETS] = {};
     int rad_set = 0;
     hipEvent_t render_done = nullptr;  // recorded on the main stream after a fused render
     // derived packed scene
@@ -503,8 +503,8 @@ int rtCreateContext(int device_index, rt_context* out) {
     c->device = device_index;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->astream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream[0], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream[1], hipStreamNonBlocking);
+    for (hipStream_t& r : c->rstream)
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&r, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->atail, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->mtail, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->gtail, hipEventDisableTiming);
@@ -604,7 +604,7 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 32);
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * RT_RAD_SETS);
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
     if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
@@ -628,7 +628,7 @@ int rtReleaseKernel(rt_kernel k) {
             (void)hipEventDestroy(pr.second);
         }
     (void)hipStreamSynchronize(k->ctx->astream);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RT_RAD_SETS; ++i) {
         if (k->rad_buf[i]) (void)hipFree(k->rad_buf[i]);
         if (k->frame_flags[i]) (void)hipFree(k->frame_flags[i]);
         if (k->rad_free[i]) (void)hipEventDestroy(k->rad_free[i]);
@@ -1007,7 +1007,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (e == hipSuccess) e = hipEventRecord(ctx->atail, as);
             if (e != hipSuccess) return map_hip(e);
             k->rad_busy[rs] = true;
-            k->rad_set ^= 1;
+            k->rad_set = (k->rad_set + 1) % RT_RAD_SETS;
             ctx->apending = true;
         }
     }

@@ -10,6 +10,12 @@
 
 #include "../../include/rt_hip.h"
 
+// fused frames: radiance sets (and render streams) used in rotation, so a render waits only for
+// the accumulation of the launch RT_RAD_SETS steps back
+#ifndef RT_RAD_SETS
+#define RT_RAD_SETS 2
+#endif
+
 struct rt_context_s {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -23,7 +29,7 @@ struct rt_context_s {
     // fused renders alternate between two streams, one per radiance set (rt_capi.cpp enqueue):
     // renders of consecutive steps are independent, so step k+1's waves take the CUs that step
     // k's draining waves free instead of waiting for its last path
-    hipStream_t rstream[2] = {};
+    hipStream_t rstream[RT_RAD_SETS] = {};
     hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
     bool apending = false;
     bool overlap = true;  // rtContextSetAccumOverlap(ctx, 0): accumulate on the main stream
