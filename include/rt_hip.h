@@ -266,7 +266,13 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   GLOBAL_OCT                        step schedule, scenes not in LDS: 1 (default) = walk the
  *                                     octant-resolved node records (32 B per node and octant) in
  *                                     HBM/L2, 0 = the 64-B node records with the top of the tree
- *                                     in LDS */
+ *                                     in LDS
+ *   PERFRAME_DEFER                    step schedule, rtEnqueueKernel: 1 = render into a radiance slot
+ *                                     and accumulate in a second launch (as a fused launch of one
+ *                                     frame), so frames queued back to back overlap (4K: Cornell
+ *                                     -3 %, bunny proxy -20 %); 0 (default) = accumulate inside the
+ *                                     render (faster when the host synchronises every frame, as the
+ *                                     reference's RenderFrame does, and for small frames) */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -286,7 +292,8 @@ enum rt_tuning {
     RT_TUNE_WF_REFILL_MIN = 15,
     RT_TUNE_WF_STREAMS_PER_CU = 16,
     RT_TUNE_WF_TOP_NODES = 17,
-    RT_TUNE_GLOBAL_OCT = 18
+    RT_TUNE_GLOBAL_OCT = 18,
+    RT_TUNE_PERFRAME_DEFER = 19
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

@@ -71,6 +71,7 @@ struct rt_kernel_s {
     int pf_parity = 0;                 // per-frame key slot read by the next launch
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
+    int pf_defer = 0;                  // per-frame step launches through radiance slots + accumulation
     int global_oct = 1;                // scenes not in LDS: walk octant records in HBM/L2 (step;
                                        // bunny proxy 1.80 -> 1.58 ms/frame, profiles/r02/goct_sweep.txt)
     // wavefront schedule: ray queues (two sets of 4 float4 planes), hit records, stream counts
@@ -726,17 +727,23 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         return RT_INVALID_MEM_OBJECT;
     rc = prepare_scene(k);
     if (rc) return rc;
-    // a per-frame launch read-modify-writes the output: after the pending accumulations
-    if (n_frames == 1) (void)qs(ctx);
     // the schedule this launch runs: the wavefront one needs a bounded bounce loop (two launches
     // per bounce), else the step schedule renders it (same bits)
     int32_t lb;
     std::memcpy(&lb, &k->u32[RT_ARG_LIGHT_BOUNCES], 4);
     const bool wf = k->sched == RT_SCHED_WAVEFRONT && lb >= 1 && lb <= rtk::kWfMaxBounces;
     const int si = wf ? rtk::kSchedWavefront : (k->sched == RT_SCHED_WAVEFRONT ? RT_SCHED_STEP : k->sched);
-    // radiance per (frame slot, work-item) + the accumulation launch: fused frames, and every
-    // wavefront render
-    const bool fused = n_frames > 1 || wf;
+    // radiance per (frame slot, work-item) + the accumulation launch: fused frames, every wavefront
+    // render, and (RT_TUNE_PERFRAME_DEFER) per-frame step launches -- then consecutive renders need
+    // not wait for each other, only the accumulations are ordered
+    // (a loop that synchronises every frame -- the reference's RenderFrame: ExecuteKernel,
+    // ReadBuffer, Finish -- gains nothing from it and pays the second launch: off by default,
+    // profiles/r02/perframe_defer.txt)
+    const bool defer = n_frames == 1 && si == RT_SCHED_STEP && k->pf_defer;
+    const bool fused = n_frames > 1 || wf || defer;
+    // a launch that accumulates in-kernel read-modify-writes the output: after the pending
+    // accumulations
+    if (!fused) (void)qs(ctx);
 
     uint64_t g0 = std::min<uint64_t>(k->range_first, global_work_size);
     uint64_t g1 = k->range_last ? std::min<uint64_t>(k->range_last, global_work_size) : global_work_size;
@@ -867,7 +874,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         wf ? (lds ? ((size_t)a.octRecords + 3 * (size_t)k->n_tris) * 16 : (size_t)a.nTop * 64) +
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && n_frames == 1 ? 4 * rtk::kFinishWaveBytes : 0) +
+                 (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
                  (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
     k->last_lds = lds;
 
@@ -902,7 +909,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch
     // start, which pays off from ~1k pixels per wave (4K) and not on small frames (512^2, 1080p)
-    if (n_frames == 1 && si == RT_SCHED_STEP &&
+    if (!fused && si == RT_SCHED_STEP &&
         (k->pf_sky == 2 || (k->pf_sky == 1 && g1 - g0 >= 1024u * 4u * grid))) {
         a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
         a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
@@ -1305,6 +1312,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_WF_STREAMS_PER_CU: if (!in(0, 64)) return RT_INVALID_VALUE; k->wf_streams_per_cu = (uint32_t)value; break;
         case RT_TUNE_WF_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->wf_top_limit = (uint32_t)value; break;
         case RT_TUNE_GLOBAL_OCT: if (!in(0, 1)) return RT_INVALID_VALUE; k->global_oct = value; break;
+        case RT_TUNE_PERFRAME_DEFER: if (!in(0, 1)) return RT_INVALID_VALUE; k->pf_defer = value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1333,6 +1341,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_WF_STREAMS_PER_CU: *value = (int)k->wf_streams_per_cu; break;
         case RT_TUNE_WF_TOP_NODES: *value = (int)k->wf_top_limit; break;
         case RT_TUNE_GLOBAL_OCT: *value = k->global_oct; break;
+        case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

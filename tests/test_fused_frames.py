@@ -228,3 +228,44 @@ def test_global_scene_walks_bunny_proxy(sched):
     want = _render(sc, W, H, 1, 4, False, tuning={"global_oct": 0})
     for goct in (0, 1):
         _same(_render(sc, W, H, 1, 4, True, sched=sched, tuning={"global_oct": goct}), want)
+
+
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_SHIPPED])
+@pytest.mark.parametrize("first,n,pre", [(0, 3, None), (3, 5, (1, 2)), (1, 9, None)])
+def test_perframe_defer(cornell, math, first, n, pre):
+    """rtEnqueueKernel with RT_TUNE_PERFRAME_DEFER: the frame renders into a radiance slot and a
+    second launch accumulates it (as a fused launch of one frame), so consecutive frames' renders
+    may overlap -- the same bits as accumulating inside the render."""
+    W, H = 256, 144
+    _same(_render(cornell, W, H, first, n, False, math, pre=pre, tuning={"perframe_defer": 1}),
+          _render(cornell, W, H, first, n, False, math, pre=pre))
+
+
+def test_perframe_defer_global_path_and_bands(cornell):
+    W, H = 240, 136
+    for kw in ({"force_global": True}, {"interleave": (3, 1)}, {"work_range": (500, W * H - 33)}):
+        _same(_render(cornell, W, H, 1, 4, False, tuning={"perframe_defer": 1}, **kw),
+              _render(cornell, W, H, 1, 4, False, **kw))
+
+
+def test_perframe_defer_stays_in_order(cornell):
+    """deferred per-frame launches mixed with fused launches, a read between them and a host
+    overwrite of the output: the bits of one in-order queue of per-frame launches"""
+    W, H = 224, 128
+    outs = []
+    for defer in (1, 0):
+        r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+        r.k.set_tuning("perframe_defer", defer)
+        for f in range(1, 4):
+            r.frame(f, light_bounces=9)
+        r.frame(4, light_bounces=9, n_frames=3)
+        mid = r.result()
+        for f in range(7, 10):
+            r.frame(f, light_bounces=9)
+        r.ctx.WriteBuffer(r.out, mid)
+        for f in range(10, 13):
+            r.frame(f, light_bounces=9)
+        outs.append((mid, r.result()))
+        r.close()
+    assert outs[0][0].tobytes() == outs[1][0].tobytes()
+    assert outs[0][1].tobytes() == outs[1][1].tobytes()
