@@ -963,10 +963,38 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + ((uint32_t)lane >> 3);
                     const uint64_t g64 = (uint64_t)row * a.width + x;
                     const bool valid = x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd;
-                    const unsigned long long vm = __ballot(valid);
+                    bool keep = valid;
+                    uint32_t sd = 0;
+                    Ray cr{};
                     if (valid) {
-                        uint32_t sd = (uint32_t)g64 + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
-                        const Ray cr = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, sd);
+                        sd = (uint32_t)g64 + frame_hash(a.frameCount + slot);  // kernel_bvh.cl:445
+                        cr = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, sd);
+                        // fused launches: a camera ray that misses the root box ends its walk at
+                        // the first visit -- Intersect finds nothing, the bounce body adds the sky
+                        // and breaks (kernel_bvh.cl:358-361), Render returns max(radiance, 0)
+                        // (:383) = K_rad: a flagged frame slot.  Decided here, on the whole tile at
+                        // once, instead of through a traversal lane, a shading batch and a finish
+                        // round (same visit, same bits, same counters; 4K Cornell 1.046 -> 1.013
+                        // ms/frame, profiles/r02/sky_early_ab.txt)
+                        if (fused && bounces > 0u) {
+                            uint32_t sk;
+                            if (oct_step<kBofs>(sc, a, 0u, ray_from_unit<M>(camPos, cr.d), kMaxDist, sk) == a.nNodes) {
+                                keep = false;
+                                if (kStats) {
+                                    ++st.rays;
+                                    ++st.visits;
+                                }
+                                const uint32_t ref = (uint32_t)g64 + slot * a.radStride;
+                                if (a.hitIds && slot + 1u == a.nFrames) {
+                                    a.hitIds[(uint32_t)g64] = -1;
+                                    a.hitT[(uint32_t)g64] = kMaxDist;
+                                }
+                                a.frameFlags[ref] = 1u;
+                            }
+                        }
+                    }
+                    const unsigned long long vm = __ballot(keep);
+                    if (keep) {
                         const uint32_t pos = lane_rank(vm);
                         ring_d[pos] = make_float4(cr.d.x, cr.d.y, cr.d.z, __uint_as_float(sd));
                         ring_g[pos] = (uint32_t)g64 + (fused ? slot * a.radStride : 0u);
