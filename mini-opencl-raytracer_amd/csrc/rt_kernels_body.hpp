@@ -976,20 +976,34 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         // once, instead of through a traversal lane, a shading batch and a finish
                         // round (same visit, same bits, same counters; 4K Cornell 1.046 -> 1.013
                         // ms/frame, profiles/r02/sky_early_ab.txt)
-                        if (fused && bounces > 0u) {
+                        // Per-frame launches with the sky key: such a pixel gets the key's
+                        // gamma step when its stored value follows the chain (else it takes the
+                        // ordinary path and the finish queue).
+                        if (bounces > 0u && (fused || a.pfKeyIn)) {
                             uint32_t sk;
                             if (oct_step<kBofs>(sc, a, 0u, ray_from_unit<M>(camPos, cr.d), kMaxDist, sk) == a.nNodes) {
-                                keep = false;
-                                if (kStats) {
-                                    ++st.rays;
-                                    ++st.visits;
+                                bool chain = fused || a.frameCount == 0u;
+                                if (!chain) {
+                                    const float4 o = a.result[(uint32_t)g64];
+                                    chain = __float_as_uint(o.x) == __float_as_uint(k_old) &&
+                                            __float_as_uint(o.y) == __float_as_uint(k_old) &&
+                                            __float_as_uint(o.z) == __float_as_uint(k_old);
                                 }
-                                const uint32_t ref = (uint32_t)g64 + slot * a.radStride;
-                                if (a.hitIds && slot + 1u == a.nFrames) {
-                                    a.hitIds[(uint32_t)g64] = -1;
-                                    a.hitT[(uint32_t)g64] = kMaxDist;
+                                if (chain) {
+                                    keep = false;
+                                    if (kStats) {
+                                        ++st.rays;
+                                        ++st.visits;
+                                    }
+                                    if (a.hitIds && slot + 1u == a.nFrames) {
+                                        a.hitIds[(uint32_t)g64] = -1;
+                                        a.hitT[(uint32_t)g64] = kMaxDist;
+                                    }
+                                    if (fused)
+                                        a.frameFlags[(uint32_t)g64 + slot * a.radStride] = 1u;
+                                    else
+                                        a.result[(uint32_t)g64] = make_float4(k_out, k_out, k_out, 0.0f);
                                 }
-                                a.frameFlags[ref] = 1u;
                             }
                         }
                     }
