@@ -875,7 +875,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * rtk::kRingWaveBytes : 0);
+                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0);
     k->last_lds = lds;
 
     const int mi = k->math;

@@ -69,9 +69,10 @@ constexpr uint32_t kFinishWaveBytes = 64u * 16u;
 #define RT_RAY_RING 1
 #endif
 // step schedule, LDS scenes: per-wave ring of camera rays generated a whole 8x8 tile at a time
-// ({dir, seed} + work-item id per slot)
+// ({dir, seed}, {invDir, sign} (fused launches) + work-item id per slot)
 constexpr uint32_t kRingSlots = 64;
-constexpr uint32_t kRingWaveBytes = kRingSlots * 16u + kRingSlots * 4u;
+constexpr uint32_t kRingWaveBytes = kRingSlots * 32u + kRingSlots * 4u;
+constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // per-frame: no invDir
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
 constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 

@@ -845,9 +845,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // (not for the octant walk over HBM/L2: bunny proxy 1.572 -> 1.536 ms/frame without it,
     // profiles/r02/goct/ring_ab_bunny.txt)
     constexpr bool kRing = kLdsScene && !kGlobalOct;
+    // fused launches also keep {invDir, sign bits} (InitRay's tail, formed at fill) per slot;
+    // per-frame launches re-form it at the pop (their finish queue leaves no LDS for it)
     float4* ring_d = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
-                     (uint32_t)(tid >> 6) * (kRingWaveBytes / 16u);
-    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + kRingSlots);
+                     (uint32_t)(tid >> 6) * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u);
+    float4* ring_i = ring_d + kRingSlots;
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (fused ? 2u : 1u) * kRingSlots);
 #else
     constexpr bool kRing = false;
     float4* ring_d = nullptr;
@@ -981,7 +984,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         // ordinary path and the finish queue).
                         if (bounces > 0u && (fused || a.pfKeyIn)) {
                             uint32_t sk;
-                            if (oct_step<kBofs>(sc, a, 0u, ray_from_unit<M>(camPos, cr.d), kMaxDist, sk) == a.nNodes) {
+                            if (oct_step<kBofs>(sc, a, 0u, cr, kMaxDist, sk) == a.nNodes) {
                                 bool chain = fused || a.frameCount == 0u;
                                 if (!chain) {
                                     const float4 o = a.result[(uint32_t)g64];
@@ -1011,6 +1014,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (keep) {
                         const uint32_t pos = lane_rank(vm);
                         ring_d[pos] = make_float4(cr.d.x, cr.d.y, cr.d.z, __uint_as_float(sd));
+                        if (fused) ring_i[pos] = make_float4(cr.inv.x, cr.inv.y, cr.inv.z, __uint_as_float(cr.sgn));
                         ring_g[pos] = (uint32_t)g64 + (fused ? slot * a.radStride : 0u);
                     }
                     rc_head = 0;
@@ -1024,7 +1028,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     const float4 e = ring_d[rc_head + rank];
                     gid = ring_g[rc_head + rank];
                     seed = __float_as_uint(e.w);
-                    ray = ray_from_unit<M>(camPos, F3{e.x, e.y, e.z});
+                    if (fused) {
+                        const float4 iv = ring_i[rc_head + rank];
+                        ray.o = camPos;
+                        ray.d = F3{e.x, e.y, e.z};
+                        ray.inv = F3{iv.x, iv.y, iv.z};
+                        ray.sgn = __float_as_uint(iv.w);
+                    } else {
+                        ray = ray_from_unit<M>(camPos, F3{e.x, e.y, e.z});
+                    }
                     radiance = f3s(0.0f);
                     beta = f3s(1.0f);
                     bounce = 0;
