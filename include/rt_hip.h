@@ -250,7 +250,10 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (0-64; default 0 =
  *                                     auto: 16 / 48 walking octant records, 8 / 48 the 64-B records)
  *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)
- *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64 (128 / 64)
+ *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64: bulk chunk
+ *                                     (512) / largest tail chunk (256; a launch uses the largest
+ *                                     power-of-two multiple of 64 up to it that gives every
+ *                                     wave >= 2.5 tail chunks)
  *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)
  *   TOP_NODES                         global path: top-of-tree nodes staged in LDS (0-1024, 384)
  *   POOL_SHADE / PARK_MIN / LOW_WORK  pool schedule thresholds (64 / 16 / 32)

@@ -62,9 +62,11 @@ struct rt_kernel_s {
     uint32_t refill_min_g = 0, shade_min_g = 0;
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
     uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
-    uint32_t chunk_pixels = 128, tail_chunk = 64;  // pixels per work-counter fetch: bulk, tail
+    // pixels per work-counter fetch: bulk, and the cap of the launch-sized tail chunk (swept on
+    // MI355X: profiles/r02/chunk_sweep.txt; 128 / 64 of round 1 left the counter at its atomic
+    // throughput once sky tiles were decided at ring fill: 4K Cornell 1.01 -> 0.79 ms/frame)
+    uint32_t chunk_pixels = 512, tail_chunk = 256;
     uint32_t bulk_percent = 80;                // share of the frame handed out in bulk chunks
-                                               // (swept on MI355X: profiles/r01/chunk_sweep.txt)
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // persistent schedules' chunk counters: [4] per render stream
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
@@ -905,6 +907,14 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.chunkSplit = tot >= 2u * waves * k->chunk_pixels
                            ? (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels)
                            : 0u;
+        // tail chunks: the largest power-of-two multiple of 64 pixels, up to tail_chunk, that still
+        // gives every wave >= 2.5 of them -- few atomics on the tail counter for large launches,
+        // fine-grained balance for small ones (4K fused 256, 4K per-frame / 1080p / 512^2 fused 128,
+        // 512^2 per-frame 64: profiles/r02/chunk_sweep.txt)
+        const uint64_t share = (tot - a.chunkSplit) / waves;
+        uint32_t tail = 64;
+        while (tail * 2u <= k->tail_chunk && (uint64_t)tail * 2u * 5u <= share * 2u) tail *= 2u;
+        a.tailChunk = tail;
     }
 
     // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch

@@ -4,7 +4,8 @@
 after another.  Prints per-rank ms per 8-frame step and the strong-scaling efficiency of the
 render alone (T1 / (N * max_r T_r)); the RCCL gather is not included.
 usage: rank_emulation.py [N ...]   (env: RT_EMU_MATH, RT_EMU_SCENE=cornell|bunny, RT_EMU_STEPS,
-       RT_EMU_FUSED=1: the 8 frames as one rtEnqueueKernelFrames call)"""
+       RT_EMU_FUSED=1: the 8 frames as one rtEnqueueKernelFrames call, RT_EMU_TUNE=name=v,name=v:
+       library tunings; RT_EMU_STEPS defaults to bench.py's 20 timed steps)"""
 import os
 import sys
 import time
@@ -23,7 +24,8 @@ if os.environ.get("RT_EMU_SCENE", "cornell") == "bunny":
     sc = proxy.bunny_proxy()
 else:
     sc = clrt.scene.cornell()
-steps = int(os.environ.get("RT_EMU_STEPS", "4"))
+steps = int(os.environ.get("RT_EMU_STEPS", "20"))
+tunes = [t.split("=") for t in os.environ.get("RT_EMU_TUNE", "").split(",") if t]
 W, H, F = 3840, 2160, 8
 t1 = None
 for n in [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]:
@@ -31,6 +33,8 @@ for n in [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]:
     for rank in range(n):
         r = HipRenderer(sc, W, H, math=math)
         r.k.set_row_interleave(n, rank)
+        for name, v in tunes:
+            r.k.set_tuning(name, int(v))
 
         def step():
             if os.environ.get("RT_EMU_FUSED", "0") == "1":
