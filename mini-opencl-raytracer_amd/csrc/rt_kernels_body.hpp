@@ -1796,8 +1796,12 @@ constexpr uint32_t kAccumTilesPerWave = RT_ACCUM_TPW;  // 8x8 tiles per wave of 
 constexpr uint32_t kAccumWgWaves = RT_ACCUM_WG_WAVES;  // waves per accumulation workgroup
 constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
 
+#ifndef RT_ACCUM_PRIO
+#define RT_ACCUM_PRIO 0  // wave priority of the accumulation launch (0: below the render's)
+#endif
 template <class M>
 __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uint32_t* key) {
+    if (RT_ACCUM_PRIO > 0) __builtin_amdgcn_s_setprio(RT_ACCUM_PRIO);
     __shared__ uint32_t queue[kAccumWgWaves][kAccumQueue];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t* q = queue[wv];
