@@ -1012,8 +1012,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (!ea || !eb) return RT_OUT_OF_RESOURCES;
             (void)hipEventRecord(ea, as);
         }
+#ifndef RT_DIAG_NO_ACCUM  // diagnostic A/B builds only (wrong images): the render without its accumulation
         e = rtk::launch_accum_frames(a, k->math, k->accum_key, as);
         if (e != hipSuccess) return map_hip(e);
+#endif
         if (k->timing) {
             (void)hipEventRecord(eb, as);
             k->pending_accum.emplace_back(ea, eb);

@@ -598,6 +598,29 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
 // first a.chunkSplit pixels, then chunks of a.tailChunk.  Large chunks keep the returning
 // atomics per frame low (one counter saturates near 90 per microsecond on MI355X); small
 // ones at the end keep the last waves from finishing alone.  Returns false when no work is left.
+// fused frames' radiance slots: written once by the render, read once by the accumulation --
+// streamed past the caches (nontemporal) where the render reads its scene through them (HBM/L2
+// scene path: bunny proxy 1.425 -> 1.404 ms/frame, profiles/r02/nt_rad_ab.txt; the LDS path
+// showed no gain for its stores)
+#ifndef RT_NT_RAD
+#define RT_NT_RAD 1
+#endif
+typedef float rad_v4f __attribute__((ext_vector_type(4)));
+template <bool kNt>
+__device__ __forceinline__ void rad_store(float4* p, float x, float y, float z) {
+    if (RT_NT_RAD && kNt)
+        __builtin_nontemporal_store(rad_v4f{x, y, z, 0.0f}, reinterpret_cast<rad_v4f*>(p));
+    else
+        *p = make_float4(x, y, z, 0.0f);
+}
+__device__ __forceinline__ float4 rad_load(const float4* p) {
+    if (RT_NT_RAD) {
+        const rad_v4f v = __builtin_nontemporal_load(reinterpret_cast<const rad_v4f*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
+
 __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
                                            uint32_t& len, bool& tail) {
     uint32_t b = 0;
@@ -904,7 +927,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     const bool skyv = __float_as_uint(radiance.x) == __float_as_uint(krad) &&
                                       __float_as_uint(radiance.y) == __float_as_uint(krad) &&
                                       __float_as_uint(radiance.z) == __float_as_uint(krad);
-                    if (!skyv) a.radBuf[gid] = make_float4(radiance.x, radiance.y, radiance.z, 0.0f);
+                    if (!skyv) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
                     a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
@@ -1727,7 +1750,7 @@ __device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gi
     FrameRad f;
 #pragma unroll
     for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
-        f.r[s] = (s < a.nFrames && !((flags >> s) & 1u)) ? a.radBuf[(size_t)s * a.radStride + gid]
+        f.r[s] = (s < a.nFrames && !((flags >> s) & 1u)) ? rad_load(a.radBuf + (size_t)s * a.radStride + gid)
                                                           : make_float4(krad, krad, krad, 0.0f);
     return f;
 }
@@ -1754,7 +1777,7 @@ __device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32
 #pragma unroll 1
     for (uint32_t s = 0; s < a.nFrames; ++s) {
         const float4 r = ((flags >> s) & 1u) ? make_float4(krad, krad, krad, 0.0f)
-                                             : a.radBuf[(size_t)s * a.radStride + gid];
+                                             : rad_load(a.radBuf + (size_t)s * a.radStride + gid);
         v = gamma_out<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
     }
     return v;
