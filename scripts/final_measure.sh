@@ -29,5 +29,7 @@ step bench_512 300 python bench.py --width 512 --height 512 --bounces 1 --frames
 step bench_bunny_perframe 300 python bench.py --scene bunny --launch per-frame --no-cpu-baseline --steps 3
 step bench_wf_cornell 300 python bench.py --sched wavefront --no-cpu-baseline --steps 5
 step bench_wf_bunny 300 python bench.py --sched wavefront --scene bunny --no-cpu-baseline --steps 3
-step rank_emulation_cornell 300 python scripts/rank_emulation.py
-step rank_emulation_bunny 400 env RT_EMU_SCENE=bunny python scripts/rank_emulation.py
+step rank_emulation_cornell 400 python scripts/rank_emulation.py
+step rank_emulation_bunny 500 env RT_EMU_SCENE=bunny python scripts/rank_emulation.py
+step rank_emulation_fused_cornell 400 env RT_EMU_FUSED=1 python scripts/rank_emulation.py
+step rank_emulation_fused_bunny 500 env RT_EMU_FUSED=1 RT_EMU_SCENE=bunny python scripts/rank_emulation.py
