@@ -904,9 +904,16 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // (bunny proxy, N = 1: -1.4 %); with few items per wave (multi-GPU ranks) it bunches a
         // costly tile's frames into the tail, so frame-major there (work_order_ab.txt)
         a.tileMajor = n_frames > 1 && (k->tile_major == 1 || (k->tile_major < 0 && !lds && tot >= 4096u * waves)) ? 1u : 0u;
-        a.chunkSplit = tot >= 2u * waves * k->chunk_pixels
-                           ? (uint32_t)(tot * k->bulk_percent / 100 / k->chunk_pixels * k->chunk_pixels)
-                           : 0u;
+        // the bulk share stops where the tail would hold less than two bulk chunks per wave: a
+        // bulk chunk (512 pixel-frames, ~0.25 ms of a wave's time at 4K) taken just before the
+        // split otherwise outlasts the tail that should even the waves out -- small launches
+        // (multi-GPU ranks: N = 8 renders 1/8 of the frame) get a larger tail (bulk 80 % -> ~37 %:
+        // emulated N = 8 rank step, Cornell 1.112 -> 1.047 ms, bunny proxy 1.694 -> 1.629 ms;
+        // profiles/r02/multigpu/n8_chunk_sweep_*.txt); full 4K launches keep 80 %
+        uint64_t bulk = tot * k->bulk_percent / 100;
+        const uint64_t reserve = 2u * waves * k->chunk_pixels;
+        bulk = std::min<uint64_t>(bulk, tot > reserve ? tot - reserve : 0u);
+        a.chunkSplit = tot >= 2u * waves * k->chunk_pixels ? (uint32_t)(bulk / k->chunk_pixels * k->chunk_pixels) : 0u;
         // tail chunks: the largest power-of-two multiple of 64 pixels, up to tail_chunk, that still
         // gives every wave >= 2.5 of them -- few atomics on the tail counter for large launches,
         // fine-grained balance for small ones (4K fused 256, 4K per-frame / 1080p / 512^2 fused 128,
