@@ -37,9 +37,9 @@ constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene pa
 #ifndef RT_TIMELINE
 #define RT_TIMELINE 0
 #endif
-// diagnostic timeline builds (-DRT_TIMELINE=1, scripts/timeline.py) write a 64-bin histogram after
+// diagnostic timeline builds (-DRT_TIMELINE=1, scripts/timeline.py) write three 64-bin histograms after
 // the primary hit ids: such a build requires hit buffers that long
-constexpr size_t kHitPad = RT_TIMELINE ? 64 : 0;
+constexpr size_t kHitPad = RT_TIMELINE ? 192 : 0;
 
 }  // namespace
 

@@ -904,6 +904,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
 #if RT_TIMELINE
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t rt_dry = 0;  // when this wave found the work counter dry
 #endif
     // diagnostic lane-utilisation counters (wave-uniform): steps / rounds and lanes served
     uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
@@ -978,6 +979,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                     if (dry) {
                         exhausted = true;
+#if RT_TIMELINE
+                        rt_dry = __builtin_amdgcn_s_memrealtime();
+#endif
                         break;
                     }
                     // one 8x8 tile, one work item per lane (chunks are whole tiles)
@@ -1300,8 +1304,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             atomicAdd(&a.stats[18], (unsigned long long)rt_end);
             atomicAdd(&a.stats[19], 1ull);
             if (a.hitIds) {
-                const uint32_t bin = min((uint32_t)((rt_end - rt_start) / 2000ull), 63u);
+                // lifetime (40 us bins), counter-dry time (40 us bins), end - dry (10 us bins)
+                const uint32_t bin = min((uint32_t)((rt_end - rt_start) / 4000ull), 63u);
                 atomicAdd(&a.hitIds[a.width * a.height + bin], 1);
+                const uint64_t dry_at = rt_dry ? rt_dry : rt_end;
+                atomicAdd(&a.hitIds[a.width * a.height + 64u + min((uint32_t)((dry_at - rt_start) / 4000ull), 63u)], 1);
+                atomicAdd(&a.hitIds[a.width * a.height + 128u + min((uint32_t)((rt_end - dry_at) / 1000ull), 63u)], 1);
             }
 #else
             atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);

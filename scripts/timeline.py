@@ -18,7 +18,7 @@ for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
         r = HipRenderer(sc, 3840, 2160, math=N.MATH_SHIPPED, stats=True)
         r.k.set_row_interleave(n, 0)
         npx = 3840 * 2160
-        hb = (r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 64) * 4), r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 64) * 4))
+        hb = (r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 192) * 4), r.ctx.create_buffer(N.MEM_READ_WRITE, (npx + 192) * 4))
         r.k.set_hit_buffers(*hb)
         r.k.reset_stats()
         if fused:
@@ -36,11 +36,13 @@ for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
               f"last wave start {last_start:.1f} us, mean wave end {mean_end:.1f} us, drain {span - mean_end:.1f} us ({(span - mean_end) / span:.1%})",
               flush=True)
         import numpy as np
-        h = np.zeros(npx + 64, np.int32)
+        h = np.zeros(npx + 192, np.int32)
         r.ctx.ReadBuffer(hb[0], h, blocking=True)
-        hist = h[npx:]
-        print("   wave lifetime histogram (20 us bins, from the first nonempty): " +
-              " ".join(str(int(x)) for x in hist[np.nonzero(hist)[0][0]:np.nonzero(hist)[0][-1] + 1]), flush=True)
+        for name, off, us in (("wave lifetime", 0, 40), ("counter dry after", 64, 40), ("wave end - dry", 128, 10)):
+            hist = h[npx + off:npx + off + 64]
+            nz = np.nonzero(hist)[0]
+            print(f"   {name} histogram ({us} us bins, bins {nz[0]}..{nz[-1]}): " +
+                  " ".join(str(int(x)) for x in hist[nz[0]:nz[-1] + 1]), flush=True)
         r.k.set_hit_buffers(None, None)
         for x in hb:
             x.release()
