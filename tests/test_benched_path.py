@@ -76,3 +76,37 @@ def test_wavefront_4k_8spp_equals_live_reference(cornell, scene_name):
     else:
         import clrt.proxy as P
         _check(P.bunny_proxy(), False, 8, sched=N.SCHED_WAVEFRONT)
+
+
+def _rank_steps(scene, period, phase, steps=3):
+    """one rank's share of an N-GPU bench (bench.py --gpus N): its interleaved 8-row bands of the
+    fused 4K 8-frame step, queued back to back as in the timed loop"""
+    r = HipRenderer(scene, W4K, H4K, math=N.MATH_SHIPPED)
+    if period > 1:
+        r.k.set_row_interleave(period, phase)
+    for _ in range(steps):
+        r.frame(1, light_bounces=9, n_frames=8)
+    r.ctx.Finish()
+    out = r.result().reshape(H4K, W4K, 4)
+    r.close()
+    return out
+
+
+@pytest.mark.parametrize("scene_name", ["cornell", "bunny"])
+def test_rank_shares_at_full_size_compose_the_benched_image(cornell, scene_name):
+    """The per-rank work of the 8-GPU bench (configs 4 and 5) at full size: ranks 0 and 7 of 8 render
+    their bands with the small-launch chunking (tail reserve) and the frame-major order of small
+    launches; their rows must be the bits of the one-GPU render (itself pinned to the reference
+    above), and they must leave every other row untouched (zero)."""
+    if scene_name == "cornell":
+        sc = cornell
+    else:
+        import clrt.proxy as P
+        sc = P.bunny_proxy()
+    full = _rank_steps(sc, 1, 0)
+    rows = np.arange(H4K)
+    for phase in (0, 7):
+        got = _rank_steps(sc, 8, phase)
+        mine = (rows // 8) % 8 == phase
+        assert got[mine].tobytes() == full[mine].tobytes(), f"rank {phase}: band rows differ"
+        assert not got[~mine].any(), f"rank {phase} wrote rows outside its bands"
