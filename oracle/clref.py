@@ -66,9 +66,13 @@ class ReferenceKernel:
                       W, H, lb, lt, sky, cam)
 
     def render(self, scene, W, H, frames=(1,), light_bounces=9, light_type=0, skybox=1.0,
-               camera=((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))):
+               camera=((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0)), result=None):
+        """KernelEntry for frames min(frames)..max(frames) into one buffer.  `result` (W*H x 4
+        float32) is the buffer's starting content (default zeros), as after earlier frames of
+        an interactive session; a new array is returned."""
         s = self._scene(scene, W, H, light_bounces, light_type, skybox, camera)
-        out = np.zeros((W * H, 4), np.float32)
+        out = np.zeros((W * H, 4), np.float32) if result is None else np.array(result, np.float32, copy=True)
+        assert out.shape == (W * H, 4)
         f0, f1 = min(frames), max(frames)
         rc = self.L.clref_render(self.h, ctypes.byref(s), f0, f1, out.ctypes.data)
         if rc != 0:

@@ -7,6 +7,42 @@ from clrt import _native as N
 DEFAULT_CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
 
 
+def _cross32(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]],
+                    np.float32)
+
+
+def reference_camera(pitch=None, yaw=None, moves=()):
+    """The camera the reference's UI hands to KernelEntry (slots 11-13, CLRaytracer.cpp:42-47).
+
+    Starts from CLCamera's defaults (CLcamera.h:8-13).  A (pitch, yaw) drag runs
+    CLCamera::Update (CLcamera.h:15-21; CLui.cpp:221-228): front = (cos yaw sin pitch,
+    sin yaw sin pitch, cos pitch) in fp32, up unchanged.  `moves` are arrow keys in order
+    (CLEngineBase.cpp:141-162): "up" pos += front, "down" pos -= front, "right"
+    pos += cross(front, up), "left" pos -= cross(front, up).  Returns (pos, front, up) as
+    Python floats of the fp32 values."""
+    pos = np.array([0.0, -25.0, 8.5], np.float32)
+    front = np.array([0.0, 1.0, 0.0], np.float32)
+    up = np.array([0.0, 0.0, 1.0], np.float32)
+    if pitch is not None:
+        p, y = np.float32(pitch), np.float32(yaw)
+        front = np.array([np.cos(y) * np.sin(p), np.sin(y) * np.sin(p), np.cos(p)], np.float32)
+    for m in moves:
+        if m == "up":
+            pos = pos + front
+        elif m == "down":
+            pos = pos - front
+        elif m == "right":
+            pos = pos + _cross32(front, up)
+        elif m == "left":
+            pos = pos - _cross32(front, up)
+        else:
+            raise ValueError(m)
+    return tuple(tuple(float(c) for c in v) for v in (pos, front, up))
+
+
 class HipRenderer:
     """One context + kernel + scene + output buffer; frames rendered on demand."""
 
