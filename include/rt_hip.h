@@ -321,9 +321,17 @@ typedef struct rt_comm_s* rt_comm;
 int rtCommGetUniqueId(void* id /* RT_COMM_ID_BYTES */);
 int rtCommInitRank(rt_context ctx, int nranks, const void* id, int rank, rt_comm* out);
 int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
+/* A world of n ranks inside this process WITHOUT RCCL: the same sharding, pack, two-slot
+ * pipelining and unpack as above, with the transfer step (grouped ncclSend/ncclRecv) replaced by
+ * device copies into the root's receive slots on the root's communicator stream.  The contexts
+ * may share one device (several ranks on one GPU), so the N > 1 gather runs where there is only
+ * one GPU.  Every gather and reduction must pass all n communicators (n_local == n). */
+int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out);
 int rtCommDestroy(rt_comm comm);
 int rtCommGetRank(rt_comm comm, int* rank, int* nranks);
-/* The kernel renders this rank's bands: rtKernelSetRowInterleave(k, nranks, rank). */
+/* The kernel renders this rank's bands: rtKernelSetRowInterleave(k, nranks, rank).  The gather's
+ * plan counts bands from image row 0, so a kernel with a work range (rtKernelSetWorkRange) is
+ * refused (RT_INVALID_OPERATION), and so is setting one on a kernel sharded this way. */
 int rtCommShardKernel(rt_comm comm, rt_kernel k);
 /* Gather the band-sharded image: every rank's bands of its `out` buffer (width x height pixels
  * of 16 bytes, rendered after rtCommShardKernel) are assembled in the root's `root_dst` (NULL =

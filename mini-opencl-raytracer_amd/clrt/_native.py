@@ -142,6 +142,7 @@ _HIP_PROTOS = {
     "rtCommGetUniqueId": (ctypes.c_int, [_vp]),
     "rtCommInitRank": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.POINTER(_vp)]),
     "rtCommInitAll": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rtCommInitLoopback": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(_vp)]),
     "rtCommDestroy": (ctypes.c_int, [_vp]),
     "rtCommGetRank": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "rtCommShardKernel": (ctypes.c_int, [_vp, _vp]),

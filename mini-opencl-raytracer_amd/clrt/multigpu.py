@@ -158,6 +158,17 @@ class Comm:
         check(N.hip_lib().rtCommInitAll(hs, n, out), "comm init all")
         return [cls(out[i], ctxs[i]) for i in range(n)]
 
+    @classmethod
+    def init_loopback(cls, ctxs) -> list["Comm"]:
+        """A world of len(ctxs) ranks in this process without RCCL (rtCommInitLoopback): the
+        transfer is a device copy, the rest of the gather is the RCCL flow; the contexts may
+        share one GPU."""
+        n = len(ctxs)
+        hs = (ctypes.c_void_p * n)(*[c.handle for c in ctxs])
+        out = (ctypes.c_void_p * n)()
+        check(N.hip_lib().rtCommInitLoopback(hs, n, out), "comm init loopback")
+        return [cls(out[i], ctxs[i]) for i in range(n)]
+
     def shard(self, kernel) -> None:
         """The kernel renders this rank's interleaved bands (rtCommShardKernel)."""
         check(self._lib.rtCommShardKernel(self.handle, kernel.handle), "shard kernel")
@@ -191,12 +202,22 @@ class Comm:
             self.handle = None
 
 
+def _rendezvous_path() -> str:
+    """Keyed by the launcher's pid (every rank of a torch.distributed.run job has the same
+    parent), MASTER_PORT, and the elastic run id + restart count: a restarted attempt (same
+    agent pid and port under --max-restarts) gets a fresh path, so no rank can read an id a
+    failed attempt left behind.  RT_COMM_ID_FILE overrides it."""
+    if os.environ.get("RT_COMM_ID_FILE"):
+        return os.environ["RT_COMM_ID_FILE"]
+    run = "".join(ch if ch.isalnum() else "_" for ch in os.environ.get("TORCHELASTIC_RUN_ID", "none"))[:64]
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    return os.path.join("/tmp", f"rt_comm_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{run}_{attempt}.id")
+
+
 def file_rendezvous(rank: int, world: int, make_id, timeout: float = 300.0) -> bytes:
     """Hand rank 0's communicator id to the other ranks of ONE node through a file (no torch,
-    no sockets): the path is keyed by the launcher's pid (every rank of a torch.distributed.run
-    job has the same parent) and MASTER_PORT; RT_COMM_ID_FILE overrides it."""
-    path = os.environ.get("RT_COMM_ID_FILE") or os.path.join(
-        "/tmp", f"rt_comm_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.id")
+    no sockets), at _rendezvous_path()."""
+    path = _rendezvous_path()
     if rank == 0:
         uid = make_id()
         tmp = f"{path}.{os.getpid()}.tmp"
@@ -219,8 +240,7 @@ def file_rendezvous(rank: int, world: int, make_id, timeout: float = 300.0) -> b
 
 
 def rendezvous_cleanup() -> None:
-    path = os.environ.get("RT_COMM_ID_FILE") or os.path.join(
-        "/tmp", f"rt_comm_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.id")
+    path = _rendezvous_path()
     try:
         os.unlink(path)
     except FileNotFoundError:

@@ -86,6 +86,7 @@ struct rt_kernel_s {
     uint32_t* wf_cnt = nullptr;        // 2 x (G + 1) words
     size_t wf_cnt_cap = 0;             // words
     uint64_t range_first = 0, range_last = 0;
+    bool comm_sharded = false;  // bands set by rtCommShardKernel: the gather's plan needs the whole frame
     rt_mem hit_ids = nullptr, hit_t = nullptr;
     bool stats = false, timing = false, force_global = false;
     unsigned long long* dstats = nullptr;  // device counters [4]
@@ -1132,8 +1133,23 @@ int rtKernelSetRowInterleave(rt_kernel k, unsigned period, unsigned phase) {
     if (period == 0 || phase >= period) return RT_INVALID_VALUE;
     k->band_period = period;
     k->band_phase = phase;
+    k->comm_sharded = false;
     return RT_SUCCESS;
 }
+
+}  // extern "C"
+
+// rtCommShardKernel: the gather's band plan counts bands from image row 0, the kernel from the
+// first row of its work range -- so a comm-sharded kernel renders whole frames only
+int rti::shard_kernel(rt_kernel k, unsigned period, unsigned phase) {
+    if (!k) return RT_INVALID_KERNEL;
+    if (k->range_first != 0 || k->range_last != 0) return RT_INVALID_OPERATION;
+    int rc = rtKernelSetRowInterleave(k, period, phase);
+    if (rc == RT_SUCCESS) k->comm_sharded = true;
+    return rc;
+}
+
+extern "C" {
 
 int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offset, size_t src_pitch,
                                      size_t width_bytes, size_t rows, void* dst, size_t dst_pitch) {
@@ -1191,6 +1207,7 @@ int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src
 int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {
     if (!k) return RT_INVALID_KERNEL;
     if (last != 0 && last < first) return RT_INVALID_VALUE;
+    if (k->comm_sharded && (first != 0 || last != 0)) return RT_INVALID_OPERATION;
     k->range_first = first;
     k->range_last = last;
     return RT_SUCCESS;

@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -78,6 +79,10 @@ int band_plan(unsigned W, unsigned H, unsigned period, unsigned phase, rt_rect* 
 struct rt_comm_s {
     rt_context ctx = nullptr;
     ncclComm_t nc = nullptr;
+    // loopback worlds (rtCommInitLoopback): no RCCL; `group` identifies the world (shared by its
+    // members) and the transfer is a device copy on the root's communicator stream
+    const void* group = nullptr;
+    hipEvent_t xfer = nullptr;  // root: the copies of one gather done
     int rank = 0, nranks = 1;
     hipStream_t cstream = nullptr;  // RCCL
     hipStream_t ustream = nullptr;  // root: unpack
@@ -104,6 +109,7 @@ int comm_streams(rt_comm c) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->unpacked[s], hipEventDisableTiming);
     }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xfer, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64 * sizeof(double));
     return map_hip(e);
 }
@@ -127,6 +133,7 @@ void release(rt_comm c) {
     for (int s = 0; s < 2; ++s)
         for (hipEvent_t ev : {c->packed[s], c->sent[s], c->unpacked[s]})
             if (ev) (void)hipEventDestroy(ev);
+    if (c->xfer) (void)hipEventDestroy(c->xfer);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -177,6 +184,11 @@ hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* s
     }
     return hipSuccess;
 }
+
+int rccl_transfer(const rt_comm* comms, int n_local, int root);
+int loopback_transfer(const rt_comm* comms, int n_local, int root);
+int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
+int check_loopback(const rt_comm* comms, int n_local);
 
 }  // namespace
 
@@ -238,6 +250,8 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
             (void)hipSetDevice(ctxs[i]->device);
             rc = comm_streams(c);
         } else {
+            (void)ncclCommDestroy(nc[i]);
+            nc[i] = nullptr;
             rc = RT_OUT_OF_HOST_MEMORY;
         }
         if (rc) {
@@ -248,6 +262,38 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
             }
             for (int j = i + 1; j < n; ++j)
                 if (nc[j]) (void)ncclCommDestroy(nc[j]);
+            return rc;
+        }
+        comms_out[i] = c;
+    }
+    return RT_SUCCESS;
+}
+
+int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
+    if (!ctxs || !comms_out || n < 1) return RT_INVALID_VALUE;
+    for (int i = 0; i < n; ++i) {
+        comms_out[i] = nullptr;
+        if (!ctxs[i]) return RT_INVALID_CONTEXT;
+    }
+    static std::atomic<uintptr_t> next_group{1};
+    const void* group = reinterpret_cast<const void*>(next_group.fetch_add(1));
+    for (int i = 0; i < n; ++i) {
+        rt_comm c = new (std::nothrow) rt_comm_s();
+        int rc = RT_OUT_OF_HOST_MEMORY;
+        if (c) {
+            c->ctx = ctxs[i];
+            c->group = group;
+            c->rank = i;
+            c->nranks = n;
+            hipError_t e = hipSetDevice(ctxs[i]->device);
+            rc = e == hipSuccess ? comm_streams(c) : map_hip(e);
+        }
+        if (rc) {
+            if (c) release(c);
+            for (int j = 0; j < i; ++j) {
+                release(comms_out[j]);
+                comms_out[j] = nullptr;
+            }
             return rc;
         }
         comms_out[i] = c;
@@ -272,7 +318,7 @@ int rtCommGetRank(rt_comm c, int* rank, int* nranks) {
 
 int rtCommShardKernel(rt_comm c, rt_kernel k) {
     if (!c) return RT_INVALID_VALUE;
-    return rtKernelSetRowInterleave(k, (unsigned)c->nranks, (unsigned)c->rank);
+    return rti::shard_kernel(k, (unsigned)c->nranks, (unsigned)c->rank);
 }
 
 int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_local, unsigned W, unsigned H,
@@ -287,6 +333,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         if (c->rank == root && root_dst && (root_dst->ctx != c->ctx || root_dst->size < img_bytes))
             return RT_INVALID_MEM_OBJECT;
     }
+    if (int rc = check_loopback(comms, n_local)) return rc;
     // phase 1: every rank (the root too) packs its bands on its context's accumulation stream
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
@@ -316,6 +363,21 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     // several GPUs).  The root posts one receive per rank, so all its links carry data at once;
     // its own bands take the same path (a send to itself, a device-local copy) -- one uniform
     // unpack, and a world of one still runs the whole RCCL flow.
+    if (comms[0]->group) {
+        int rc = loopback_transfer(comms, n_local, root);
+        if (rc) return rc;
+    } else {
+        int rc = rccl_transfer(comms, n_local, root);
+        if (rc) return rc;
+    }
+    return finish_gather(comms, n_local, root, root_dst, outs);
+}
+
+}  // extern "C"
+
+namespace {
+
+int rccl_transfer(const rt_comm* comms, int n_local, int root) {
     int rc = map_nccl(ncclGroupStart());
     if (rc) return rc;
     for (int i = 0; i < n_local && rc == RT_SUCCESS; ++i) {
@@ -329,8 +391,36 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     }
     const int rc_end = map_nccl(ncclGroupEnd());
     if (rc) return rc;
-    if (rc_end) return rc_end;
-    // phase 3: the root unpacks every rank's bands into the destination
+    return rc_end;
+}
+
+// loopback world: the root's communicator stream copies every rank's staging slot into its
+// receive slots (after each rank's pack), then every rank's communicator stream waits for those
+// copies -- the same stream and event chain as the RCCL send/receive above.
+int loopback_transfer(const rt_comm* comms, int n_local, int root) {
+    rt_comm R = nullptr;
+    for (int i = 0; i < n_local; ++i)
+        if (comms[i]->rank == root) R = comms[i];
+    hipError_t e = hipSetDevice(R->ctx->device);
+    for (int i = 0; i < n_local && e == hipSuccess; ++i) {
+        rt_comm c = comms[i];
+        e = hipStreamWaitEvent(R->cstream, c->packed[c->slot], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(static_cast<uint8_t*>(R->parts[R->slot]) + (size_t)c->rank * R->stage_bytes,
+                               c->stage[c->slot], c->stage_bytes, hipMemcpyDeviceToDevice, R->cstream);
+    }
+    if (e == hipSuccess) e = hipEventRecord(R->xfer, R->cstream);
+    for (int i = 0; i < n_local && e == hipSuccess; ++i) {
+        rt_comm c = comms[i];
+        if (c == R) continue;
+        e = hipSetDevice(c->ctx->device);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, R->xfer, 0);
+    }
+    return map_hip(e);
+}
+
+// phase 3: the root unpacks every rank's bands into the destination
+int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs) {
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         rt_context ctx = c->ctx;
@@ -360,11 +450,54 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     return RT_SUCCESS;
 }
 
+// a loopback world's calls must name all its members, each once
+int check_loopback(const rt_comm* comms, int n_local) {
+    const void* g = comms[0]->group;
+    if (!g) {
+        for (int i = 1; i < n_local; ++i)
+            if (comms[i]->group) return RT_INVALID_VALUE;
+        return RT_SUCCESS;
+    }
+    if (n_local != comms[0]->nranks) return RT_INVALID_VALUE;
+    uint64_t seen = 0;
+    for (int i = 0; i < n_local; ++i) {
+        if (comms[i]->group != g || comms[i]->rank >= 64) return RT_INVALID_VALUE;
+        const uint64_t bit = 1ull << comms[i]->rank;
+        if (seen & bit) return RT_INVALID_VALUE;
+        seen |= bit;
+    }
+    return RT_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
 int rtCommAllReduceF64(const rt_comm* comms, int n_local, double* values, int count, int op) {
     if (!comms || n_local < 1 || !values || count < 1 || count > 64) return RT_INVALID_VALUE;
     if (op != RT_COMM_SUM && op != RT_COMM_MAX) return RT_INVALID_VALUE;
-    for (int i = 0; i < n_local; ++i) {
+    for (int i = 0; i < n_local; ++i)
         if (!comms[i]) return RT_INVALID_VALUE;
+    if (int rc = check_loopback(comms, n_local)) return rc;
+    if (comms[0]->group) {
+        // loopback world: every member is here, so the reduction is over these rows, after the
+        // members' communicator streams (earlier gathers) have drained, as RCCL's would
+        for (int i = 0; i < n_local; ++i) {
+            hipError_t e = hipSetDevice(comms[i]->ctx->device);
+            if (e == hipSuccess) e = hipStreamSynchronize(comms[i]->cstream);
+            if (e != hipSuccess) return map_hip(e);
+        }
+        for (int j = 0; j < count; ++j) {
+            double acc = values[j];
+            for (int i = 1; i < n_local; ++i) {
+                const double v = values[(size_t)i * count + j];
+                acc = op == RT_COMM_SUM ? acc + v : std::max(acc, v);
+            }
+            for (int i = 0; i < n_local; ++i) values[(size_t)i * count + j] = acc;
+        }
+        return RT_SUCCESS;
+    }
+    for (int i = 0; i < n_local; ++i) {
         hipError_t e = hipSetDevice(comms[i]->ctx->device);
         if (e == hipSuccess)
             e = hipMemcpyAsync(comms[i]->scratch, values + (size_t)i * count, count * sizeof(double),

@@ -78,4 +78,7 @@ inline hipStream_t qs(rt_context ctx) {
     return ctx->stream;
 }
 
+// rtCommShardKernel's interleave (rt_capi.cpp): refused for a kernel with a work range
+int shard_kernel(rt_kernel k, unsigned period, unsigned phase);
+
 }  // namespace rti

@@ -94,7 +94,7 @@ def _rank_steps(scene, period, phase, steps=3):
 
 @pytest.mark.parametrize("scene_name", ["cornell", "bunny"])
 def test_rank_shares_at_full_size_compose_the_benched_image(cornell, scene_name):
-    """The per-rank work of the 8-GPU bench (configs 4 and 5) at full size: ranks 0 and 7 of 8 render
+    """The per-rank work of the 8-GPU bench (configs 4 and 5) at full size: every rank of 8 renders
     their bands with the small-launch chunking (tail reserve) and the frame-major order of small
     launches; their rows must be the bits of the one-GPU render (itself pinned to the reference
     above), and they must leave every other row untouched (zero)."""
@@ -105,7 +105,7 @@ def test_rank_shares_at_full_size_compose_the_benched_image(cornell, scene_name)
         sc = P.bunny_proxy()
     full = _rank_steps(sc, 1, 0)
     rows = np.arange(H4K)
-    for phase in (0, 7):
+    for phase in range(8):
         got = _rank_steps(sc, 8, phase)
         mine = (rows // 8) % 8 == phase
         assert got[mine].tobytes() == full[mine].tobytes(), f"rank {phase}: band rows differ"

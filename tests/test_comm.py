@@ -7,8 +7,10 @@ path: pack on the accumulation stream, a send/receive to itself, unpack): the ga
 is byte-identical to the rendered one, through ncclCommInitRank and ncclCommInitAll, gathered
 into a separate buffer or into the output itself, pipelined over back-to-back steps, after
 per-frame launches; and bench.py's own N > 1 flow (--force-dist --check-gather) in a fresh
-process.  Worlds of 2..8 ranks need more GPUs than the test box has: the driver's 8-GPU bench
-runs them; the band arithmetic for them is the CPU part here and tests/test_multigpu_gloo.py.
+process.  Worlds of 2..8 ranks run on the one GPU as a loopback world (rtCommInitLoopback: every
+rank its own context, the RCCL transfer replaced by device copies, the rest of the gather as is),
+at the bench's full 4K 8-spp size; the RCCL transfer between N > 1 GPUs is the driver's 8-GPU
+bench.  The band arithmetic is also the CPU part here and tests/test_multigpu_gloo.py.
 """
 import os
 import subprocess
@@ -45,6 +47,32 @@ def test_native_plan_rejects_bad_arguments():
     for args in [(0, 8, 1, 0), (8, 0, 1, 0), (8, 8, 0, 0), (8, 8, 2, 2)]:
         with pytest.raises(clrt.RTError):
             mg.native_pack_plan(*args)
+
+
+def test_rendezvous_path_is_per_attempt(monkeypatch):
+    """A torchrun restart keeps the agent pid and MASTER_PORT; the id file must still change, so
+    no rank reads a communicator id a failed attempt left behind."""
+    monkeypatch.delenv("RT_COMM_ID_FILE", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job/1")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    a = mg._rendezvous_path()
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    b = mg._rendezvous_path()
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job2")
+    c = mg._rendezvous_path()
+    assert len({a, b, c}) == 3 and "/" not in os.path.basename(a)
+    monkeypatch.setenv("RT_COMM_ID_FILE", "/tmp/x.id")
+    assert mg._rendezvous_path() == "/tmp/x.id"
+    uid = bytes(range(N.COMM_ID_BYTES))
+    monkeypatch.setenv("RT_COMM_ID_FILE", "")
+    monkeypatch.delenv("RT_COMM_ID_FILE")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "7")
+    monkeypatch.setenv("MASTER_PORT", str(40000 + os.getpid() % 1000))
+    assert mg.file_rendezvous(0, 2, lambda: uid) == uid
+    assert mg.file_rendezvous(1, 2, None, timeout=5) == uid
+    mg.rendezvous_cleanup()
+    assert not os.path.exists(mg._rendezvous_path())
 
 
 # ---- GPU -----------------------------------------------------------------------------------
@@ -158,3 +186,148 @@ def test_bench_rccl_flow_world_of_one(tmp_path):
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "byte-identical" in p.stdout
+
+
+# ---- N > 1 on one GPU: the loopback world (rtCommInitLoopback) ----------------------------------
+# The same sharding, pack on the accumulation stream, two-slot pipelining, per-rank receive slots
+# parts[s] + q*stage_bytes, per-rank unpack plans (with the short last band) and event chain
+# across ranks as the RCCL world -- only the grouped ncclSend/ncclRecv is replaced by device
+# copies.  Every rank is its own context on the one GPU of the test box.  (The RCCL transfer for
+# N > 1 itself needs N GPUs: the driver's 8-GPU bench.)
+def _scene(cornell, name):
+    if name == "cornell":
+        return cornell
+    import clrt.proxy as P
+    return P.bunny_proxy()
+
+
+def _unsharded(ctx, scene, W, H, steps):
+    bufs, out, k = _setup(ctx, scene, W, H)
+    for step in range(steps):
+        k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+        ctx.ExecuteKernelFrames(k, W * H, 8)
+    img = _read(ctx, out, W * H)
+    for b in bufs + [out]:
+        b.release()
+    k.release()
+    return img
+
+
+def _loopback_gather(scene, n, W, H, steps, root=0, into_out=False):
+    """n ranks, each its own context: `steps` fused 8-frame renders of its bands (frames 1+8s ..
+    8+8s, accumulating), each followed at once by the pipelined gather to `root`, as bench.py's
+    timed loop queues them.  Returns (gathered image, every rank's own output buffer)."""
+    import clrt
+    ctxs = [clrt.CLContext(0) for _ in range(n)]
+    comms = mg.Comm.init_loopback(ctxs)
+    assert [(c.rank, c.nranks) for c in comms] == [(q, n) for q in range(n)]
+    setups = [_setup(ctx, scene, W, H) for ctx in ctxs]
+    for c, (_, _, k) in zip(comms, setups):
+        c.shard(k)
+    outs = [s[1] for s in setups]
+    dst = None if into_out else ctxs[root].create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    for step in range(steps):
+        for ctx, (_, _, k) in zip(ctxs, setups):
+            k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+            ctx.ExecuteKernelFrames(k, W * H, 8)
+        mg.Comm.gather_bands(comms, outs, W, H, root=root, dst=dst)
+    for ctx in ctxs:
+        ctx.Finish()
+    gathered = _read(ctxs[root], dst or outs[root], W * H)
+    shares = [_read(ctx, o, W * H) for ctx, o in zip(ctxs, outs)]
+    v = mg.Comm.allreduce(comms, [[float(q), 1.0] for q in range(n)], N.COMM_SUM)
+    assert (v == [[n * (n - 1) / 2, float(n)]] * n).all()
+    mg.Comm.barrier(comms)
+    for c in comms:
+        c.destroy()
+    for (bufs, out, k) in setups:
+        for b in bufs + [out]:
+            b.release()
+        k.release()
+    if dst:
+        dst.release()
+    for ctx in ctxs:
+        ctx.release()
+    return gathered, shares
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_loopback_gather_4k_8spp_pipelined_equals_unsharded(cornell, n):
+    """The 4K 8-spp bench workload on n ranks: three pipelined steps, the gathered image
+    byte-identical to the unsharded render (itself pinned to the reference kernel in
+    test_benched_path.py), and every rank's buffer holding exactly its bands."""
+    import clrt
+    W, H = 3840, 2160
+    ctx = clrt.CLContext(0)
+    full = _unsharded(ctx, cornell, W, H, 3)
+    ctx.release()
+    gathered, shares = _loopback_gather(cornell, n, W, H, 3)
+    assert gathered.tobytes() == full.tobytes()
+    rows = np.arange(H)
+    f = full.reshape(H, W, 4)
+    for q, s in enumerate(shares):
+        s = s.reshape(H, W, 4)
+        mine = (rows // 8) % n == q
+        assert s[mine].tobytes() == f[mine].tobytes(), f"rank {q}/{n}: band rows differ"
+        assert not s[~mine].any(), f"rank {q}/{n} wrote rows outside its bands"
+
+
+@pytest.mark.gpu
+def test_loopback_gather_bunny_n8(cornell):
+    """Config 5's shape (the 70k-triangle proxy, octant walk over HBM/L2) at N = 8."""
+    import clrt
+    sc = _scene(cornell, "bunny")
+    W, H = 3840, 2160
+    ctx = clrt.CLContext(0)
+    full = _unsharded(ctx, sc, W, H, 2)
+    ctx.release()
+    gathered, _ = _loopback_gather(sc, 8, W, H, 2)
+    assert gathered.tobytes() == full.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,n,root,into_out", [(1277, 731, 3, 2, False), (640, 37, 8, 5, True),
+                                                  (333, 9, 2, 1, True), (64, 8, 4, 0, False)])
+def test_loopback_gather_ragged(cornell, W, H, n, root, into_out):
+    """Odd sizes (short last band, ranks with no band at all), a root other than 0, gathering
+    into the root's own output buffer."""
+    import clrt
+    ctx = clrt.CLContext(0)
+    full = _unsharded(ctx, cornell, W, H, 3)
+    ctx.release()
+    gathered, _ = _loopback_gather(cornell, n, W, H, 3, root=root, into_out=into_out)
+    assert gathered.tobytes() == full.tobytes()
+
+
+@pytest.mark.gpu
+def test_loopback_calls_must_name_the_whole_world(cornell):
+    import clrt
+    ctxs = [clrt.CLContext(0) for _ in range(3)]
+    comms = mg.Comm.init_loopback(ctxs)
+    setups = [_setup(ctx, cornell, 64, 64) for ctx in ctxs]
+    with pytest.raises(clrt.RTError):
+        mg.Comm.gather_bands(comms[:2], [s[1] for s in setups[:2]], 64, 64)
+    with pytest.raises(clrt.RTError):
+        mg.Comm.gather_bands([comms[0], comms[0], comms[1]], [s[1] for s in setups], 64, 64)
+    with pytest.raises(clrt.RTError):
+        mg.Comm.allreduce(comms[1:], [[1.0], [2.0]])
+    # a comm-sharded kernel renders whole frames: work ranges are refused both ways
+    k = setups[0][2]
+    comms[0].shard(k)
+    with pytest.raises(clrt.RTError) as e:
+        k.set_work_range(0, 64 * 8)
+    assert e.value.code == -59  # CL_INVALID_OPERATION
+    k2 = setups[1][2]
+    k2.set_work_range(64, 64 * 20)
+    with pytest.raises(clrt.RTError) as e:
+        comms[1].shard(k2)
+    assert e.value.code == -59
+    for c in comms:
+        c.destroy()
+    for (bufs, out, kk) in setups:
+        for b in bufs + [out]:
+            b.release()
+        kk.release()
+    for ctx in ctxs:
+        ctx.release()
