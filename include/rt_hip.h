@@ -154,7 +154,8 @@ int rtKernelSetSchedule(rt_kernel k, int sched);
  * build on the host quickly.  Permutes `tris` in place into leaf order and writes the
  * depth-first CLLinearBVHNode[] into `nodes` (capacity >= (2*n_tris - 1) * 48 bytes), count
  * in *n_nodes -- the node contract of CLBVHnode.cpp:161-183, so the buffers bind to
- * KernelEntry as they are.  The tree is not the host SAH tree (hit IDs may differ where
+ * KernelEntry as they are (the tree is the first *n_nodes records; the rest of a 2n-1 buffer is
+ * ignored, see rtValidateBVH).  The tree is not the host SAH tree (hit IDs may differ where
  * triangles tie). */
 int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, rt_mem nodes,
                size_t* n_nodes);
@@ -232,11 +233,14 @@ int rtContextGetAccumStream(rt_context ctx, void** hip_stream);
 int rtContextGetDevice(rt_context ctx, int* device_index);
 
 /* Host-only check (no GPU) of a flattened BVH against the contract KernelEntry relies on
- * (CLBVHnode.cpp:161-183): interior node i has children i+1 and offset > i+1, both < n_nodes,
- * axis <= 2; leaves [offset, offset + nPrimitives) lie within the n_tris triangles; every node
- * but the root has exactly one parent (one tree, every node reachable).  Every launch runs it
- * on the bound arrays first (RT_INVALID_MEM_OBJECT, never a GPU walk).  *depth = the deepest
- * leaf's depth. */
+ * (CLBVHnode.cpp:161-183).  The tree is the prefix [0, end) of the n_nodes records, `end` = one
+ * past the leaf that node 0's chain of second children reaches (depth-first layout); records
+ * past it are never read (by the reference's walk from node 0 either), so a node buffer may be
+ * larger than its tree -- e.g. rtBuildBVH's buffer of 2n-1 records holding `count`.  Within the
+ * tree: interior node i has children i+1 and offset > i+1, both < end, axis <= 2; leaves
+ * [offset, offset + nPrimitives) lie within the n_tris triangles; every node but the root has
+ * exactly one parent (one tree, every node reachable).  Every launch runs it on the bound
+ * arrays first (RT_INVALID_MEM_OBJECT, never a GPU walk).  *depth = the deepest leaf's depth. */
 int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
 
 /* Scheduling parameters of the persistent schedules (extension; no effect on results, only on

@@ -149,14 +149,24 @@ int host_bytes(rt_mem m, std::vector<uint8_t>& tmp, const uint8_t** out) {
     return RT_SUCCESS;
 }
 
-// Validate the flattened BVH (CLBVHnode.cpp:161-183 contract) and return its depth.  Every
-// node is checked, reachable or not (the skip/record builders below walk all of them), and
-// the array must be exactly one tree: each node but the root has exactly one parent.  Since a
-// parent's index is smaller than its children's, that makes every node reachable from node 0
-// and the skip-pointer walk a finite depth-first order (a child shared by two parents would
-// make it loop).
-int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* depth_out) {
+// Validate the flattened BVH (CLBVHnode.cpp:161-183 contract) and return its depth and its
+// node count.  The tree is the prefix [0, end) of the array: in the depth-first layout (first
+// child = parent + 1, second child after the first child's subtree) the root's subtree ends
+// after the leaf its chain of second children reaches.  Nodes past `end` are never read -- by
+// the reference's walk from node 0 either -- so a buffer may be larger than the tree it holds
+// (rtBuildBVH writes `count` nodes into a buffer of 2n-1).  Within the tree every node is
+// checked and each one but the root must have exactly one parent; since a parent's index is
+// smaller than its children's, that makes every node reachable from node 0 and the
+// skip-pointer walk a finite depth-first order (a child shared by two parents would make it
+// loop).
+int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* depth_out, uint32_t* n_used) {
     if (n == 0) return RT_INVALID_MEM_OBJECT;
+    uint32_t last = 0;  // the root's chain of second children (offsets strictly increase)
+    while (nd[last].nPrimitives == 0) {
+        if (nd[last].offset <= last || nd[last].offset >= n) return RT_INVALID_MEM_OBJECT;
+        last = nd[last].offset;
+    }
+    n = last + 1;
     std::vector<int> depth(n, -1);
     std::vector<uint8_t> parents(n, 0);
     depth[0] = 0;
@@ -178,6 +188,7 @@ int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* dept
         }
     }
     *depth_out = max_depth;
+    *n_used = n;
     // The reference's 64-entry stack (kernel_bvh.cl:181) would overflow past depth 64; the
     // stackless walk here has no such limit, so deeper trees are rendered, not rejected.
     return RT_SUCCESS;
@@ -361,7 +372,7 @@ int prepare_scene(rt_kernel k) {
         mm->size < sizeof(rt_cl_material))
         return RT_INVALID_MEM_OBJECT;
     const uint32_t nt = (uint32_t)(tm->size / sizeof(rt_cl_triangle));
-    const uint32_t nn = (uint32_t)(nm->size / sizeof(rt_cl_bvh_node));
+    const uint32_t n_buf = (uint32_t)(nm->size / sizeof(rt_cl_bvh_node));
     const uint32_t nmat = (uint32_t)(mm->size / sizeof(rt_cl_material));
     const bool tris_stale = k->packed_for_tris != tm || k->packed_tris_gen != tm->generation;
     const bool nodes_stale = k->packed_for_nodes != nm || k->packed_nodes_gen != nm->generation;
@@ -375,7 +386,8 @@ int prepare_scene(rt_kernel k) {
     rc = host_bytes(nm, tmp_n, &nb);
     if (rc) return rc;
     int depth = 0;
-    rc = check_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn, nt, &depth);
+    uint32_t nn = 0;  // the tree's nodes: a prefix of the buffer
+    rc = check_nodes(reinterpret_cast<const rt_cl_bvh_node*>(nb), n_buf, nt, &depth, &nn);
     if (rc) return rc;
     const rt_cl_triangle* tr = reinterpret_cast<const rt_cl_triangle*>(tb);
     for (uint32_t i = 0; i < nt; ++i)
@@ -1314,7 +1326,8 @@ int rtContextGetDevice(rt_context ctx, int* d) {
 int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth) {
     if (!nodes || n_nodes == 0 || n_nodes >= (1u << 30) || n_tris >= (1ull << 32)) return RT_INVALID_VALUE;
     int d = 0;
-    int rc = check_nodes(static_cast<const rt_cl_bvh_node*>(nodes), (uint32_t)n_nodes, (uint32_t)n_tris, &d);
+    uint32_t used = 0;
+    int rc = check_nodes(static_cast<const rt_cl_bvh_node*>(nodes), (uint32_t)n_nodes, (uint32_t)n_tris, &d, &used);
     if (rc == RT_SUCCESS && depth) *depth = d;
     return rc;
 }

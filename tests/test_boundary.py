@@ -106,18 +106,30 @@ def test_validate_bvh_rejects_shared_child():
     assert e.value.code == -38
 
 
-def test_validate_bvh_rejects_unreachable_interior_with_bad_offset():
-    """An unreachable interior node whose offset is out of range is still rejected (the
-    record builders walk every node)."""
+def test_validate_bvh_orphans_and_trailing_records():
+    """Inside the tree (the prefix up to the leaf node 0's chain of second children reaches) an
+    unreachable node is rejected; records after the tree are never read, by the reference's
+    walk from node 0 either, so they are ignored whatever they hold (rtBuildBVH's node buffer
+    has 2n-1 records for a tree of `count`)."""
     from clrt import _native as N
-    nd = np.zeros(4, N.NODE_DTYPE)
+    nd = np.zeros(5, N.NODE_DTYPE)
+    _interior(nd[0], 3)
+    _leaf(nd[1], 0, 1)
+    _leaf(nd[2], 1, 1)  # inside the tree [0, 4) but nobody's child
+    _leaf(nd[3], 1, 1)
+    _interior(nd[4], 99)
+    with pytest.raises(clrt.RTError) as e:
+        N.validate_bvh(nd, 2)
+    assert e.value.code == -38
+    nd = np.zeros(6, N.NODE_DTYPE)
     _interior(nd[0], 2)
     _leaf(nd[1], 0, 1)
     _leaf(nd[2], 1, 1)
-    _interior(nd[3], 99)
-    with pytest.raises(clrt.RTError):
-        N.validate_bvh(nd, 2)
-    _leaf(nd[3], 0, 1)  # well-formed but orphaned
+    _interior(nd[3], 99)  # past the tree: garbage allowed
+    _interior(nd[4], 1)
+    assert N.validate_bvh(nd, 2) == 1
+    nd = np.zeros(3, N.NODE_DTYPE)
+    _interior(nd[0], 7)  # the root's second child past the buffer
     with pytest.raises(clrt.RTError):
         N.validate_bvh(nd, 2)
 

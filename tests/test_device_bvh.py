@@ -105,3 +105,48 @@ def test_device_bvh_bunny_matches_sah_image():
     same = (a.view(np.uint32) == b.view(np.uint32)).all(axis=-1).mean()
     print(f"device build of {raw.triangles.shape[0]} triangles: {build_s * 1e3:.1f} ms incl. transfers; "
           f"same face {agree:.5f}; {same:.4f} of pixels bit-identical to the SAH tree's image")
+
+
+@pytest.mark.parametrize("max_prims", [1, 4])
+def test_device_bvh_buffers_bind_to_kernel_entry_as_they_are(oracle_mod, max_prims):
+    """rt_hip.h's flow for rtBuildBVH: the triangle and node buffers it wrote are bound to
+    KernelEntry directly -- the node buffer keeps its 2n-1 records (the tree is the first
+    `count`, the rest unused) -- and the render equals the oracle's on the tree read back."""
+    import clrt
+    tris, mats = _file_order_cornell()
+    n = tris.shape[0]
+    W, H = 128, 96
+    ctx = clrt.CLContext(0)
+    tb = ctx.create_buffer(N.MEM_READ_WRITE | N.MEM_COPY_HOST_PTR, tris.nbytes, tris)
+    nb = ctx.create_buffer(N.MEM_READ_WRITE, (2 * n - 1) * N.NODE_DTYPE.itemsize)
+    mb = ctx.create_buffer(N.MEM_READ_ONLY | N.MEM_COPY_HOST_PTR, mats.nbytes, mats)
+    count = ctx.BuildBVH(tb, n, max_prims, nb)
+    assert (max_prims == 1) == (count == 2 * n - 1)
+    out = ctx.create_buffer(N.MEM_WRITE_ONLY, W * H * 16)
+    k = clrt.CLKernel(ctx)
+    for slot, b in ((N.BUFFER_OUT, out), (N.BUFFER_SCENE, tb), (N.BUFFER_NODE, nb), (N.BUFFER_MATERIAL, mb)):
+        k.set_buffer(slot, b)
+    k.set_math_mode(N.MATH_PINNED)
+    k.set_int(N.WIDTH, W)
+    k.set_int(N.HEIGHT, H)
+    k.set_int(N.LIGHT_BOUNCES, 4)
+    k.set_int(N.LIGHT_TYPE, 0)
+    k.set_float(N.SKYBOX_INTENSITY, 1.0)
+    k.set_uint(N.FRAME_SEED, 0)
+    for slot, v in zip((N.CAMERA_POS, N.CAMERA_FRONT, N.CAMERA_UP), ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))):
+        k.set_float3(slot, v)
+    k.set_uint(N.FRAME_COUNT, 1)
+    ctx.ExecuteKernel(k, W * H)
+    got = np.zeros((W * H, 4), np.float32)
+    ctx.ReadBuffer(out, got, blocking=True)
+    t_dev = np.empty_like(tris)
+    n_dev = np.empty(count, N.NODE_DTYPE)
+    ctx.ReadBuffer(tb, t_dev, blocking=True)
+    ctx.ReadBuffer(nb, n_dev, n_dev.nbytes, blocking=True)
+    for b in (tb, nb, mb, out):
+        b.release()
+    k.release()
+    ctx.release()
+    sc = S.Scene(t_dev, n_dev, mats, max_prims)
+    want, _, _, _ = oracle_mod.render(sc, W, H, frame_count=1, light_bounces=4, threads=16)
+    assert (rgb(got).view(np.uint32) == rgb(want).view(np.uint32)).all()
