@@ -807,7 +807,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if (tilesY == 0) return RT_SUCCESS;
     }
     const uint64_t n_tiles = tilesY * a.tilesX;
-    if (n_tiles * 64 > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
+    if (n_tiles * 64 > 0xfff00000ull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
     a.workCounter = k->work_counter;
     a.chunkPixels = k->chunk_pixels;
@@ -826,7 +826,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     if (fused) {
         // fused frames: radiance slots indexed by global work-item id (the lane packs
         // slot * g1 + gid into 32 bits); tiles x frames work items
-        if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xffffffffull)
+        // (work items stay below 2^32 - 2^20: the work-stealing ranges add a few tiles past
+        // their end in 32-bit fields)
+        if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xfff00000ull)
             return RT_INVALID_GLOBAL_WORK_SIZE;
         const size_t need = (size_t)n_frames * g1;
         const int rs = ctx->overlap ? k->rad_set : 0;
@@ -890,7 +892,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0);
+                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
+                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
 
     const int mi = k->math;

@@ -73,6 +73,12 @@ constexpr uint32_t kFinishWaveBytes = 64u * 16u;
 constexpr uint32_t kRingSlots = 64;
 constexpr uint32_t kRingWaveBytes = kRingSlots * 32u + kRingSlots * 4u;
 constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // per-frame: no invDir
+// step schedule, LDS scenes: per workgroup, each wave's remaining chunk {next, end} (64-bit word
+// per wave), from which its siblings take single tiles once the work counter is dry
+#ifndef RT_STEAL
+#define RT_STEAL 1
+#endif
+constexpr uint32_t kStealBytes = RT_STEAL ? 4u * 8u + 32u : 0u;  // (padded to whole float4s)
 // pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
 constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 

@@ -673,7 +673,8 @@ __global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
     F3 radiance = f3s(0.0f), beta = f3s(1.0f);
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
+    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
     bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
 
@@ -818,6 +819,45 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 
 __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__popcll(__ballot(p)); }
 
+// The next 8x8 tile of work for the calling wave (wave-uniform; returns false when there is none).
+// Work stealing within the workgroup: a wave's chunk from the work counter is a {next, end} range
+// in LDS (steal[wave], one 64-bit word) it takes its tiles from one at a time; once the counter is
+// dry, the wave takes single tiles from its siblings' ranges instead of ending while they still
+// hold whole chunks.  64-bit LDS atomics hand out every tile exactly once, whoever takes it, so
+// the results cannot change (seeds follow the work item, kernel_bvh.cl:445).  Emulated N = 8 rank
+// step -4 %, per-frame 4K launches -5 % (profiles/r03/steal_ab.txt).
+__device__ __forceinline__ bool take_tile(const KernelArgs& a, unsigned long long* steal, uint32_t me, uint32_t lane,
+                                          uint32_t total, uint32_t& chunk_base, uint32_t& chunk_len, bool& chunk_tail,
+                                          bool& dry, uint32_t& unit) {
+    if (!dry) {
+        unsigned long long old = 0;
+        if (lane == 0) old = atomicAdd(&steal[me], 64ull);
+        old = __shfl(old, 0, 64);
+        if ((uint32_t)old < (uint32_t)(old >> 32)) {
+            unit = (uint32_t)old;
+            return true;
+        }
+        if (next_chunk(a, total, lane, chunk_base, chunk_len, chunk_tail)) {
+            if (lane == 0)
+                (void)atomicExch(&steal[me], ((unsigned long long)(chunk_base + chunk_len) << 32) |
+                                                 (unsigned long long)(chunk_base + 64u));
+            unit = chunk_base;
+            return true;
+        }
+        dry = true;
+    }
+    for (uint32_t k = 1; k < 4u; ++k) {
+        unsigned long long old = 0;
+        if (lane == 0) old = atomicAdd(&steal[(me + k) & 3u], 64ull);
+        old = __shfl(old, 0, 64);
+        if ((uint32_t)old < (uint32_t)(old >> 32)) {
+            unit = (uint32_t)old;
+            return true;
+        }
+    }
+    return false;
+}
+
 template <class M, bool kLdsScene, bool kStats, bool kBofs = false, bool kGlobalOct = false>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
@@ -825,17 +865,28 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // (second stream), which then only fill the slots the render leaves idle (bunny proxy -1.5 %;
     // profiles/r01/render_priority_ab.txt); traversal steps raise it further (below)
     if (!kLdsScene) __builtin_amdgcn_s_setprio(1);
+    // frames fused into this launch (rtEnqueueKernelFrames): work item = (frame slot, pixel);
+    // a finished path stores its radiance in radBuf[slot][gid] for accum_frames, and the lane's
+    // `gid` register then holds slot * radStride + gid
+    const bool fused = a.radBuf != nullptr;
+    // the waves' remaining chunks (work stealing, take_tile): empty ranges before anyone looks
+    unsigned long long* steal = nullptr;
+    if (RT_STEAL) {
+        extern __shared__ __attribute__((aligned(16))) float4 smem_s[];
+        constexpr bool kRingLds = RT_RAY_RING && kLdsScene && !kGlobalOct;
+        steal = reinterpret_cast<unsigned long long*>(
+            smem_s + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
+            (kRingLds ? 4u * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u) : 0u));
+        if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
+    }
     const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
+    if (RT_STEAL && kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
     const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
     const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
     const uint32_t bounces = (uint32_t)a.lightBounces;
-    // frames fused into this launch (rtEnqueueKernelFrames): work item = (frame slot, pixel);
-    // a finished path stores its radiance in radBuf[slot][gid] for accum_frames, and the lane's
-    // `gid` register then holds slot * radStride + gid
-    const bool fused = a.radBuf != nullptr;
     const uint32_t total = a.nTiles * 64u * (fused ? a.nFrames : 1u);
     // the radiance of a primary miss, max(1 * 0.5*skybox + 0, 0) per component (kernel_bvh.cl:360, :383)
     const float krad = M::max(madd<M>(1.0f, 0.5f * a.skyboxIntensity, 0.0f), 0.0f);
@@ -896,9 +947,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     uint32_t leaf_i = 0u, leaf_end = 0;
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
+    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
     bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
+    [[maybe_unused]] uint32_t tile_unit = 0, tile_used = 64;  // wave-uniform (work stealing, HBM/L2 scene paths)
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
@@ -971,13 +1024,20 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 const unsigned long long idle = __ballot(state == kIdle);
                 if (idle == 0ull) break;
                 if (rc_n == 0u) {
+                    uint32_t unit = 0;  // the tile's first work item in the work order (wave-uniform)
+#if RT_STEAL
+                    if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
+                                   chunk_tail, dry, unit)) {
+#else
                     if (!dry && chunk_used >= chunk_len) {
                         if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail))
                             dry = true;
                         else
                             chunk_used = 0;
                     }
+                    unit = chunk_base + chunk_used;
                     if (dry) {
+#endif
                         exhausted = true;
 #if RT_TIMELINE
                         rt_dry = __builtin_amdgcn_s_memrealtime();
@@ -985,7 +1045,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         break;
                     }
                     // one 8x8 tile, one work item per lane (chunks are whole tiles)
-                    uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform
+                    uint32_t tile = unit >> 6;  // wave-uniform
                     const uint32_t slot = fused ? tile / a.nTiles : 0u;  // frame-major (LDS scenes)
                     tile -= slot * a.nTiles;
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
@@ -1046,7 +1106,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                     rc_head = 0;
                     rc_n = (uint32_t)__popcll(vm);
+#if !RT_STEAL
                     chunk_used += 64u;
+#endif
                     continue;
                 }
                 const uint32_t rank = lane_rank(idle);
@@ -1087,6 +1149,18 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             while (!kRing && !exhausted) {
                 const unsigned long long idle = __ballot(state == kIdle);
                 if (idle == 0ull) break;
+#if RT_STEAL
+                // tile_unit: the current tile's first work item, tile_used of its 64 handed out
+                if (tile_used >= 64u) {
+                    if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
+                                   chunk_tail, dry, tile_unit)) {
+                        exhausted = true;
+                        break;
+                    }
+                    tile_used = 0;
+                }
+                const uint32_t used = tile_used, unit = tile_unit;
+#else
                 if (chunk_used >= chunk_len) {
                     if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
                         exhausted = true;
@@ -1094,12 +1168,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                     chunk_used = 0;
                 }
+                const uint32_t used = chunk_used & 63u, unit = (chunk_base + chunk_used) & ~63u;
+#endif
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
+                const uint32_t take = min((uint32_t)__popcll(idle), 64u - used);  // within one 8x8 tile
                 if (state == kIdle && rank < take) {
-                    const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                    uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
+                    const uint32_t w = used + rank;  // chunks are whole 8x8 tiles
+                    uint32_t tile = unit >> 6;  // wave-uniform (scalar division)
                     // fused work order: frame-major (all tiles of a frame, then the next: cheap
                     // sky tiles and costly tiles mix in every wave), or -- large launches on
                     // scenes read from HBM/L2 (a.tileMajor) -- tile-major, a tile's frames back
@@ -1140,7 +1216,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         }
                     }
                 }
+#if RT_STEAL
+                tile_used += take;
+#else
                 chunk_used += take;
+#endif
             }
         }
         uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1464,7 +1544,8 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
     uint32_t cur = 0, leaf_i = 0, leaf_end = 0;
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_used = 0, chunk_len = 0;  // wave-uniform
+    uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
+    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
     bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
