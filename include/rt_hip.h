@@ -279,7 +279,9 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     frame), so frames queued back to back overlap (4K: Cornell
  *                                     -3 %, bunny proxy -20 %); 0 (default) = accumulate inside the
  *                                     render (faster when the host synchronises every frame, as the
- *                                     reference's RenderFrame does, and for small frames) */
+ *                                     reference's RenderFrame does, and for small frames)
+ *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
+ *                                     as many as fit, default; fewer = fewer waves per SIMD) */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -300,7 +302,8 @@ enum rt_tuning {
     RT_TUNE_WF_STREAMS_PER_CU = 16,
     RT_TUNE_WF_TOP_NODES = 17,
     RT_TUNE_GLOBAL_OCT = 18,
-    RT_TUNE_PERFRAME_DEFER = 19
+    RT_TUNE_PERFRAME_DEFER = 19,
+    RT_TUNE_MAX_BLOCKS = 20
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

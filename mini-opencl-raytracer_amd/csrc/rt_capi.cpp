@@ -74,6 +74,7 @@ struct rt_kernel_s {
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
     int pf_defer = 0;                  // per-frame step launches through radiance slots + accumulation
+    int max_blocks = 0;                // persistent grid: workgroups per CU (0 = as many as fit)
     int global_oct = 1;                // scenes not in LDS: walk octant records in HBM/L2 (step;
                                        // bunny proxy 1.80 -> 1.58 ms/frame, profiles/r02/goct_sweep.txt)
     // wavefront schedule: ray queues (two sets of 4 float4 planes), hit records, stream counts
@@ -905,7 +906,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct);
         k->occ_smem[si][mi][lds][k->stats][var] = smem;
     }
-    uint64_t grid = (uint64_t)occ * (uint64_t)ctx->num_cus;
+    uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
     // (wavefront extend: 8 waves per workgroup)
     grid = std::min<uint64_t>(grid, si == RT_SCHED_TILES ? n_tiles
@@ -1359,6 +1360,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_PARK_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->park_min = (uint32_t)value; break;
         case RT_TUNE_LOW_WORK: if (!in(1, 128)) return RT_INVALID_VALUE; k->low_work = (uint32_t)value; break;
         case RT_TUNE_TILE_MAJOR: if (!in(-1, 1)) return RT_INVALID_VALUE; k->tile_major = value; break;
+        case RT_TUNE_MAX_BLOCKS: if (!in(0, 64)) return RT_INVALID_VALUE; k->max_blocks = value; break;
         case RT_TUNE_PERFRAME_SKY: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_sky = value; break;
         case RT_TUNE_WF_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->wf_refill_min = (uint32_t)value; break;
         case RT_TUNE_WF_STREAMS_PER_CU: if (!in(0, 64)) return RT_INVALID_VALUE; k->wf_streams_per_cu = (uint32_t)value; break;
@@ -1388,6 +1390,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_PARK_MIN: *value = (int)k->park_min; break;
         case RT_TUNE_LOW_WORK: *value = (int)k->low_work; break;
         case RT_TUNE_TILE_MAJOR: *value = k->tile_major; break;
+        case RT_TUNE_MAX_BLOCKS: *value = k->max_blocks; break;
         case RT_TUNE_PERFRAME_SKY: *value = k->pf_sky; break;
         case RT_TUNE_WF_REFILL_MIN: *value = (int)k->wf_refill_min; break;
         case RT_TUNE_WF_STREAMS_PER_CU: *value = (int)k->wf_streams_per_cu; break;
