@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--no-accum-overlap", action="store_true",
                    help="fused frames: accumulate on the main stream (rtContextSetAccumOverlap 0)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-drop-in", action="store_true",
+                   help="skip the extra per-frame (drop-in RenderFrame loop) measurement reported beside "
+                        "the fused headline at N = 1")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--gather-sync", action="store_true",
                    help="N>1: wait for each step's gather before queueing the next step (no pipelining)")
@@ -222,6 +225,37 @@ def cpu_baseline(scene, args, rays_per_step):
                       f"/root/reference/kernel_bvh.cl compiled unmodified for x86-64 (pinned builtins), "
                       f"{threads} threads ({int(rays_per_step)} rays, {dt:.2f} s wall)",
             "ms_per_frame": dt * 1e3 / args.frames}
+
+
+def drop_in(r, args, rays_per_step, steps=3):
+    """The drop-in path beside the fused headline: the same step as the reference's RenderFrame
+    loop issues it -- one rtEnqueueKernel (ExecuteKernel) per frame -- (a) queued back to back,
+    (b) with RenderFrame's per-frame ReadBuffer of the W*H*16-B image + Finish (CLRaytracer.cpp:
+    57-59; PCIe read-back inside, so never the headline)."""
+    k = make_kernel(r.ctx, r.bufs, r.out, args)
+    W, H, F = args.width, args.height, args.frames
+
+    def frames(readback, host):
+        for f in range(1, F + 1):
+            k.set_uint(N.FRAME_COUNT, f)
+            r.ctx.ExecuteKernel(k, W * H)
+            if readback:
+                r.ctx.ReadBuffer(r.out, host, blocking=True)
+    host = np.empty((W * H, 4), np.float32)
+    frames(False, host)
+    r.finish()
+    out = {"launch": "per frame (rtEnqueueKernel, the reference's RenderFrame loop)"}
+    for name, rb, n in (("queued", False, steps), ("with_readback", True, 1)):
+        t0 = time.perf_counter()
+        for _ in range(n):
+            frames(rb, host)
+        r.finish()
+        dt = (time.perf_counter() - t0) / n
+        out[name] = {"ms_per_frame": round(dt * 1e3 / F, 4), "value": round(rays_per_step / dt / 1e6, 1),
+                     "unit": "Mrays/s"}
+    out["with_readback"]["note"] = f"ReadBuffer of {W * H * 16 / 1e6:.1f} MB + Finish after every frame, as RenderFrame does"
+    k.release()
+    return out
 
 
 def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts, tile_px):
@@ -390,6 +424,8 @@ def main():
     }
     if check:
         line["check_gather"] = check
+    if world == 1 and comm is None and args.launch == "fused" and not args.no_drop_in:
+        line["drop_in"] = drop_in(r, args, rays_per_step)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(scene, args, pinned_rays(r, args))
     print(json.dumps(line))
