@@ -250,7 +250,7 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  * RT_INVALID_VALUE.
  *   REFILL_MIN / SHADE_MIN            step schedule, LDS scenes: finish + refill when this many
  *                                     lanes are free (1-64, default 6); shade when this many are
- *                                     ready (1-64, default 44)
+ *                                     ready (1-64, default 48)
  *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (0-64; default 0 =
  *                                     auto: 16 / 48 walking octant records, 8 / 48 the 64-B records)
  *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)

@@ -55,8 +55,10 @@ struct rt_kernel_s {
     int math = RT_MATH_SHIPPED;  // the reference as its host builds it (rt_hip.h)
     int sched = RT_SCHED_STEP;
     // step schedule thresholds (lanes), swept on MI355X: LDS scenes (camera-ray ring)
-    // profiles/r01/threshold_sweep_ring.txt; scenes read from HBM/L2 keep 8 / 48
-    uint32_t refill_min = 6, shade_min = 44;
+    // profiles/r01/threshold_sweep_ring.txt, shading at 48 since work stealing (44 -> 48: fused
+    // -0.3 %, per-frame -0.5 %, profiles/r03/shade_threshold_sweep.txt); scenes read from HBM/L2
+    // keep 8 / 48
+    uint32_t refill_min = 6, shade_min = 48;
     // scenes read from HBM/L2: 0 = auto (64-B node records 8 / 48; octant records 16 / 48,
     // profiles/r02/goct_sweep.txt)
     uint32_t refill_min_g = 0, shade_min_g = 0;
