@@ -180,6 +180,7 @@ def kernel_source_hash() -> str:
     h = hashlib.sha1()
     files = sorted(glob.glob(os.path.join(REPO, "mini-opencl-raytracer_amd", "csrc", "rt_kernels*"))
                    + [os.path.join(REPO, "mini-opencl-raytracer_amd", "csrc", "rt_math.hpp"),
+                      os.path.join(REPO, "mini-opencl-raytracer_amd", "csrc", "rt_capi.cpp"),  # launch parameters
                       os.path.join(REPO, "include", "rt_pinned_math.h"),
                       os.path.join(REPO, "include", "rt_cl_types.h"),
                       os.path.join(REPO, "mini-opencl-raytracer_amd", "Makefile")])
