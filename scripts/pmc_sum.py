@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Sum rocprofv3 --pmc counters per kernel over all of its dispatches, plus the trace's total
-duration per kernel.  usage: pmc_sum.py DIR  (DIR from scripts/pmc_kernels.sh)"""
+duration per kernel.  usage: pmc_sum.py DIR [--all]  (DIR from scripts/pmc_kernels.sh or
+scripts/pmc_variants.sh; --all: also kernels without SQ_INSTS_VALU)"""
 import csv
 import glob
 import os
@@ -8,7 +9,7 @@ import sys
 from collections import defaultdict
 
 
-def main(d):
+def main(d, show_all=False):
     acc = defaultdict(lambda: defaultdict(float))
     n = defaultdict(lambda: defaultdict(int))
     for f in glob.glob(os.path.join(d, "p_*", "**", "*counter_collection.csv"), recursive=True):
@@ -21,7 +22,7 @@ def main(d):
         for row in csv.DictReader(open(f)):
             dur[row["Kernel_Name"]] += (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
     for k, cs in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_INSTS_VALU", 0)):
-        if cs.get("SQ_INSTS_VALU", 0) < 1e6:
+        if cs.get("SQ_INSTS_VALU", 0) < 1e6 and not show_all:
             continue
         print(f"{k[:100]}  dispatches {max(n[k].values())}  trace ms {dur.get(k, 0):.3f}")
         v = cs.get("SQ_INSTS_VALU", 0)
@@ -36,4 +37,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], "--all" in sys.argv[2:])
