@@ -242,7 +242,7 @@ def drop_in(r, args, rays_per_step, steps=3):
             r.ctx.ExecuteKernel(k, W * H)
             if readback:
                 r.ctx.ReadBuffer(r.out, host, blocking=True)
-    host = np.empty((W * H, 4), np.float32)
+    host = np.ones((W * H, 4), np.float32)  # resident pages, as the reference's long-lived image vector
     frames(False, host)
     r.finish()
     out = {"launch": "per frame (rtEnqueueKernel, the reference's RenderFrame loop)"}

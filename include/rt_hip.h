@@ -276,10 +276,14 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     in LDS
  *   PERFRAME_DEFER                    step schedule, rtEnqueueKernel: 1 = render into a radiance slot
  *                                     and accumulate in a second launch (as a fused launch of one
- *                                     frame), so frames queued back to back overlap (4K: Cornell
- *                                     -3 %, bunny proxy -20 %); 0 (default) = accumulate inside the
- *                                     render (faster when the host synchronises every frame, as the
- *                                     reference's RenderFrame does, and for small frames)
+ *                                     frame), so frames queued back to back overlap (4K Cornell
+ *                                     1.11 -> 0.92 ms/frame); 0 = accumulate inside the render
+ *                                     (faster when the host synchronises every frame, as the
+ *                                     reference's RenderFrame does, and for small frames);
+ *                                     2 (default) = defer a launch of at least PERFRAME_DEFER_MIN
+ *                                     work items exactly when the previous per-frame render of the
+ *                                     kernel is still running (the host is queueing frames)
+ *   PERFRAME_DEFER_MIN                work items from which PERFRAME_DEFER 2 defers (default 4 Mi)
  *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
  *                                     as many as fit, default; fewer = fewer waves per SIMD) */
 enum rt_tuning {
@@ -303,7 +307,8 @@ enum rt_tuning {
     RT_TUNE_WF_TOP_NODES = 17,
     RT_TUNE_GLOBAL_OCT = 18,
     RT_TUNE_PERFRAME_DEFER = 19,
-    RT_TUNE_MAX_BLOCKS = 20
+    RT_TUNE_MAX_BLOCKS = 20,
+    RT_TUNE_PERFRAME_DEFER_MIN = 21
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

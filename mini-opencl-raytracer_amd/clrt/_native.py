@@ -76,7 +76,8 @@ TUNING = {"refill_min": 0, "shade_min": 1, "refill_min_global": 2, "shade_min_gl
           "step_weight_node": 4, "step_weight_leaf": 5, "chunk_pixels": 6, "tail_chunk": 7,
           "bulk_percent": 8, "top_nodes": 9, "pool_shade": 10, "park_min": 11, "low_work": 12,
           "tile_major": 13, "perframe_sky": 14, "wf_refill_min": 15, "wf_streams_per_cu": 16,
-          "wf_top_nodes": 17, "global_oct": 18, "perframe_defer": 19, "max_blocks": 20}
+          "wf_top_nodes": 17, "global_oct": 18, "perframe_defer": 19, "max_blocks": 20,
+          "perframe_defer_min": 21}
 
 
 class Stats(ctypes.Structure):

@@ -75,7 +75,9 @@ struct rt_kernel_s {
     int pf_parity = 0;                 // per-frame key slot read by the next launch
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
-    int pf_defer = 0;                  // per-frame step launches through radiance slots + accumulation
+    int pf_defer = 2;                  // per-frame step launches through radiance slots + accumulation
+                                       // (0 never, 1 always, 2 while the previous one still runs)
+    uint32_t pf_defer_min = 4u << 20;  // ... (2) from this many work items per launch
     int max_blocks = 0;                // persistent grid: workgroups per CU (0 = as many as fit)
     int global_oct = 1;                // scenes not in LDS: walk octant records in HBM/L2 (step;
                                        // bunny proxy 1.80 -> 1.58 ms/frame, profiles/r02/goct_sweep.txt)
@@ -111,6 +113,7 @@ struct rt_kernel_s {
     bool rad_busy[RT_RAD_SETS] = {};
     int rad_set = 0;
     hipEvent_t render_done = nullptr;  // recorded on the main stream after a fused render
+    uint64_t pf_waits = ~0ull;         // ctx->host_waits at the previous per-frame step launch
     // derived packed scene
     rt_mem packed_for_tris = nullptr, packed_for_nodes = nullptr, checked_mats = nullptr;
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
@@ -754,10 +757,20 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // radiance per (frame slot, work-item) + the accumulation launch: fused frames, every wavefront
     // render, and (RT_TUNE_PERFRAME_DEFER) per-frame step launches -- then consecutive renders need
     // not wait for each other, only the accumulations are ordered
-    // (a loop that synchronises every frame -- the reference's RenderFrame: ExecuteKernel,
-    // ReadBuffer, Finish -- gains nothing from it and pays the second launch: off by default,
-    // profiles/r02/perframe_defer.txt)
-    const bool defer = n_frames == 1 && si == RT_SCHED_STEP && k->pf_defer;
+    // A loop that synchronises every frame -- the reference's RenderFrame: ExecuteKernel,
+    // ReadBuffer, Finish -- gains nothing from it and pays the second launch, and so do small
+    // frames; frames queued back to back gain (4K Cornell 1.11 -> 0.92 ms/frame).  So by default
+    // (PERFRAME_DEFER 2) a large launch defers exactly when the previous per-frame render of this
+    // kernel has not finished yet: the host is queueing, not waiting
+    // (profiles/r03/perframe_defer_auto.txt).  "Queueing" = no host wait on the context (rtFinish,
+    // a blocking read or write) since the previous per-frame launch: no GPU-side query, which
+    // would itself cost the read-back loop (an event after every render: 3.63 -> 4.07 ms/frame).
+    bool defer = false;
+    if (n_frames == 1 && si == RT_SCHED_STEP && k->pf_defer) {
+        defer = k->pf_defer == 1 ||
+                (k->pf_defer == 2 && k->pf_waits == ctx->host_waits && global_work_size >= k->pf_defer_min);
+        k->pf_waits = ctx->host_waits;
+    }
     const bool fused = n_frames > 1 || wf || defer;
     // a launch that accumulates in-kernel read-modify-writes the output: after the pending
     // accumulations
@@ -1090,6 +1103,12 @@ int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in
     return RT_SUCCESS;
 }
 
+// the host waits for the context's queue
+static hipError_t host_wait(rt_context ctx) {
+    ++ctx->host_waits;
+    return hipStreamSynchronize(qs(ctx));
+}
+
 int rtEnqueueReadBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, size_t size, void* dst) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
@@ -1097,7 +1116,7 @@ int rtEnqueueReadBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, s
     if (!dst || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
     hipError_t e = hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
                                   hipMemcpyDeviceToHost, qs(ctx));
-    if (e == hipSuccess && blocking) e = hipStreamSynchronize(qs(ctx));
+    if (e == hipSuccess && blocking) e = host_wait(ctx);
     return map_hip(e);
 }
 
@@ -1111,7 +1130,7 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, 
     ++m->generation;
     hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(m->dptr) + offset, src, size,
                                   hipMemcpyHostToDevice, qs(ctx));
-    if (e == hipSuccess && blocking) e = hipStreamSynchronize(qs(ctx));
+    if (e == hipSuccess && blocking) e = host_wait(ctx);
     return map_hip(e);
 }
 
@@ -1127,7 +1146,7 @@ int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem m, size_t offset, size_t
 int rtFinish(rt_context ctx) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
-    return map_hip(hipStreamSynchronize(qs(ctx)));
+    return map_hip(host_wait(ctx));
 }
 
 int rtKernelSetMathMode(rt_kernel k, int mode) {
@@ -1368,7 +1387,8 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_WF_STREAMS_PER_CU: if (!in(0, 64)) return RT_INVALID_VALUE; k->wf_streams_per_cu = (uint32_t)value; break;
         case RT_TUNE_WF_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->wf_top_limit = (uint32_t)value; break;
         case RT_TUNE_GLOBAL_OCT: if (!in(0, 1)) return RT_INVALID_VALUE; k->global_oct = value; break;
-        case RT_TUNE_PERFRAME_DEFER: if (!in(0, 1)) return RT_INVALID_VALUE; k->pf_defer = value; break;
+        case RT_TUNE_PERFRAME_DEFER: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_defer = value; break;
+        case RT_TUNE_PERFRAME_DEFER_MIN: if (value < 0) return RT_INVALID_VALUE; k->pf_defer_min = (uint32_t)value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1399,6 +1419,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_WF_TOP_NODES: *value = (int)k->wf_top_limit; break;
         case RT_TUNE_GLOBAL_OCT: *value = k->global_oct; break;
         case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
+        case RT_TUNE_PERFRAME_DEFER_MIN: *value = (int)k->pf_defer_min; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

@@ -32,6 +32,9 @@ struct rt_context_s {
     hipStream_t rstream[RT_RAD_SETS] = {};
     hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
     bool apending = false;
+    // host waits on the queue (rtFinish, blocking reads / writes): a per-frame launch with no wait
+    // since the previous one is being queued back to back (automatic per-frame deferral)
+    uint64_t host_waits = 0;
     bool overlap = true;  // rtContextSetAccumOverlap(ctx, 0): accumulate on the main stream
     // rtContextSetReadbackOnAccumStream: buffer -> pointer rect copies go to astream, right after
     // the accumulation they read, so the main stream runs on into the next render

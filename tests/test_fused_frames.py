@@ -253,9 +253,10 @@ def test_perframe_defer_stays_in_order(cornell):
     overwrite of the output: the bits of one in-order queue of per-frame launches"""
     W, H = 224, 128
     outs = []
-    for defer in (1, 0):
+    for defer in (1, 2, 0):
         r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
         r.k.set_tuning("perframe_defer", defer)
+        r.k.set_tuning("perframe_defer_min", 0)  # (2: defer whenever the previous frame still runs)
         for f in range(1, 4):
             r.frame(f, light_bounces=9)
         r.frame(4, light_bounces=9, n_frames=3)
@@ -267,5 +268,25 @@ def test_perframe_defer_stays_in_order(cornell):
             r.frame(f, light_bounces=9)
         outs.append((mid, r.result()))
         r.close()
-    assert outs[0][0].tobytes() == outs[1][0].tobytes()
-    assert outs[0][1].tobytes() == outs[1][1].tobytes()
+    for o in outs[:2]:
+        assert o[0].tobytes() == outs[2][0].tobytes()
+        assert o[1].tobytes() == outs[2][1].tobytes()
+
+
+@pytest.mark.parametrize("math", [N.MATH_PINNED, N.MATH_SHIPPED])
+def test_perframe_defer_auto_queued(cornell, math):
+    """PERFRAME_DEFER 2 (the default): frames queued back to back defer while the previous render
+    still runs, frames after a host wait do not -- whatever the mix, the bits of accumulating in
+    the render"""
+    W, H = 320, 180
+    want = _render(cornell, W, H, 1, 12, False, math, tuning={"perframe_defer": 0})
+    r = HipRenderer(cornell, W, H, math=math)
+    r.k.set_tuning("perframe_defer_min", 0)
+    assert r.k.get_tuning("perframe_defer") == 2
+    for f in range(1, 13):
+        r.frame(f, light_bounces=9)
+        if f in (4, 9):
+            r.ctx.Finish()
+    got = r.result()
+    r.close()
+    assert got.tobytes() == want[0].tobytes(), f"{(got != want[0]).any(axis=1).sum()} pixels differ"
