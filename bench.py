@@ -291,6 +291,11 @@ def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts,
     if "hbm_bytes_per_launch" in e:
         rl["traffic"] = int(e["hbm_bytes_per_launch"])
         rl["hbm_frac"] = round(e["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    if "TA_TA_BUSY_sum" in e and e.get("GRBM_GUI_ACTIVE"):
+        # vector-memory address unit (TA) busy share of the launch: TA cycles summed over the 256
+        # CUs against the busy cycles summed over the 8 XCDs -- the HBM/L2 octant walk's binding
+        # resource (VALU issue is not: DESIGN.md section 5)
+        rl["ta_busy"] = round(e["TA_TA_BUSY_sum"] / 256.0 / (e["GRBM_GUI_ACTIVE"] / 8.0), 4)
     rl["pmc"] = {"file": "profiles/pmc.json", "key": key, "valu_insts_per_launch": int(insts),
                  "kernel_ms_in_pmc_pass": e.get("kernel_ms"), "source_hash": e.get("source_hash"),
                  "stale": e.get("source_hash") != src}

@@ -17,6 +17,7 @@ step write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/p_write -o run
 step sq1 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/p_sq1 -o run -- $B
 step sq2 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d $OUT/p_sq2 -o run -- $B
 step wrq rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/p_wrq -o run -- $B
-python scripts/pmc_record.py $OUT/trace $OUT/p_fetch $OUT/p_write $OUT/p_sq1 $OUT/p_sq2 $OUT/p_wrq -- --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in "$@" > $OUT/record.txt
+step ta rocprofv3 --pmc TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum --output-format csv -d $OUT/p_ta -o run -- $B
+python scripts/pmc_record.py $OUT/trace $OUT/p_fetch $OUT/p_write $OUT/p_sq1 $OUT/p_sq2 $OUT/p_wrq $OUT/p_ta -- --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in "$@" > $OUT/record.txt
 cp profiles/pmc.json $OUT/pmc.json
 tail -3 $OUT/record.txt
