@@ -244,6 +244,7 @@ def drop_in(r, args, rays_per_step, steps=3):
                 r.ctx.ReadBuffer(r.out, host, blocking=True)
     host = np.ones((W * H, 4), np.float32)  # resident pages, as the reference's long-lived image vector
     frames(False, host)
+    r.ctx.ReadBuffer(r.out, host, blocking=True)  # (first read-back into these pages, untimed)
     r.finish()
     out = {"launch": "per frame (rtEnqueueKernel, the reference's RenderFrame loop)"}
     for name, rb, n in (("queued", False, steps), ("with_readback", True, 1)):
