@@ -788,7 +788,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #define RT_GPHASE 1  // global path: phase priorities (traversal 3 / shading 1) instead of a fixed 1
 #endif
 #ifndef RT_NODE_BURST
-#define RT_NODE_BURST 6
+#define RT_NODE_BURST 7  // LDS walk (6 before work stealing; 5 / 8 slower: profiles/r03/burst_sweep.txt)
 #endif
 // diagnostic (stats variant, scripts/timeline.py): wave start/end timeline instead of the
 // lane-wait counters
@@ -802,7 +802,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 
 // the same for scenes read from HBM/L2 (global path)
 #ifndef RT_GNODE_BURST
-#define RT_GNODE_BURST RT_NODE_BURST
+#define RT_GNODE_BURST 6
 #endif
 #ifndef RT_GTRI_BURST
 #define RT_GTRI_BURST RT_TRI_BURST
