@@ -109,6 +109,7 @@ struct rt_kernel_s {
     float4* rad_buf[RT_RAD_SETS] = {};
     uint8_t* frame_flags[RT_RAD_SETS] = {};
     size_t rad_buf_cap[RT_RAD_SETS] = {};  // float4 slots
+    size_t flag_cap[RT_RAD_SETS] = {};     // frame-flag bytes
     hipEvent_t rad_free[RT_RAD_SETS] = {};  // recorded on astream after the accumulation reading the set
     bool rad_busy[RT_RAD_SETS] = {};
     int rad_set = 0;
@@ -847,8 +848,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if ((uint64_t)n_frames * g1 > 0xffffffffull || n_tiles * 64 * n_frames > 0xfff00000ull)
             return RT_INVALID_GLOBAL_WORK_SIZE;
         const size_t need = (size_t)n_frames * g1;
+        // frame flags: a byte per (slot, work item), or a 64-bit word per (slot, tile) (flagTiles)
+        const size_t fneed = std::max<size_t>(need, (size_t)n_frames * n_tiles * 8u);
         const int rs = ctx->overlap ? k->rad_set : 0;
-        if (k->rad_buf_cap[rs] < need) {
+        if (k->rad_buf_cap[rs] < need || k->flag_cap[rs] < fneed) {
             // the set may still be read by an accumulation in flight
             hipError_t me = hipStreamSynchronize(ctx->astream);
             if (me != hipSuccess) return map_hip(me);
@@ -857,14 +860,16 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             k->rad_buf[rs] = nullptr;
             k->frame_flags[rs] = nullptr;
             k->rad_buf_cap[rs] = 0;
+            k->flag_cap[rs] = 0;
             me = hipMalloc(&k->rad_buf[rs], need * sizeof(float4));
-            if (me == hipSuccess) me = hipMalloc(&k->frame_flags[rs], need);
+            if (me == hipSuccess) me = hipMalloc(&k->frame_flags[rs], fneed);
             if (me == hipSuccess && !k->rad_free[rs])
                 me = hipEventCreateWithFlags(&k->rad_free[rs], hipEventDisableTiming);
             if (me == hipSuccess && !k->render_done)
                 me = hipEventCreateWithFlags(&k->render_done, hipEventDisableTiming);
             if (me != hipSuccess) return map_hip(me);
             k->rad_buf_cap[rs] = need;
+            k->flag_cap[rs] = fneed;
         }
         if (ctx->overlap && !k->hit_ids && !wf) {
             // the set's own render stream, after everything queued on the main stream so far
@@ -911,6 +916,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
                  (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
+    // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
+    // fill; the other fused renders write a byte per path at its end
+    a.flagTiles = fused && !wf && si == RT_SCHED_STEP && lds && RT_RAY_RING ? 1u : 0u;
 
     const int mi = k->math;
     const bool bofs = lds && a.octB == rtk::kOctB;

@@ -46,7 +46,11 @@ struct KernelArgs {
     // rtEnqueueKernelFrames (step schedule): frames frameCount .. frameCount + nFrames - 1 in one
     // launch; radiance per (frame slot, gid) in radBuf[slot * radStride + gid] (null: one frame)
     float4* radBuf;
-    uint8_t* frameFlags;                // [slot * radStride + gid]: 1 = radiance (K_rad x3), not in radBuf
+    // primary-miss flags: 1 = radiance (K_rad x3), not in radBuf.  flagTiles 0: one byte per
+    // [slot * radStride + gid]; flagTiles 1 (renders that generate camera rays a whole 8x8 tile at
+    // a time, the ray ring): one 64-bit word per [slot * nTiles + tile], bit = pixel's lane in the tile
+    uint8_t* frameFlags;
+    uint32_t flagTiles;
     uint32_t nFrames, radStride;
     uint32_t tileMajor;                 // fused: work items ordered (tile, frame) instead of (frame, tile)
     // per-frame launches (step schedule): sky-pixel shortcut key, chained launch to launch --

@@ -1097,11 +1097,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             }
                         }
                     }
-                    // fused: the tile's frame flags, all written here, at once (1: decided as a
-                    // primary miss above) -- a flag byte per path written at its end went out
-                    // as partial lines: 4K Cornell writes 0.94 -> 0.81 GB per launch, -0.3 %
-                    // time (profiles/r03/write_traffic.txt)
-                    if (fused && valid) a.frameFlags[(uint32_t)g64 + slot * a.radStride] = keep ? 0u : 1u;
+                    // fused: the tile's frame flags, all written here, at once, as one 64-bit
+                    // word per (frame slot, tile) -- bit = lane, 1: decided as a primary miss
+                    // above -- at [unit / 64] (frame-major order: slot * nTiles + tile).  A flag
+                    // byte per path written at its end, then 8 flag bytes per tile row here, went
+                    // out as partial lines: 4K Cornell writes 0.94 -> 0.81 -> 0.69 GB per launch
+                    // (profiles/r03/write_traffic.txt)
+                    const unsigned long long skym = __ballot(valid && !keep);
+                    if (fused && lane == 0)
+                        reinterpret_cast<unsigned long long*>(a.frameFlags)[unit >> 6] = skym;
                     const unsigned long long vm = __ballot(keep);
                     if (keep) {
                         const uint32_t pos = lane_rank(vm);
@@ -1840,6 +1844,14 @@ __device__ __forceinline__ uint32_t load_flags(const KernelArgs& a, uint32_t gid
         if (s < a.nFrames) fl |= (uint32_t)a.frameFlags[(size_t)s * a.radStride + gid] << s;
     return fl;
 }
+// the same bits from the per-tile words (flagTiles): the tile's F words are wave-uniform loads
+__device__ __forceinline__ uint32_t load_tile_flags(const KernelArgs& a, uint32_t tile, uint32_t lane) {
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(a.frameFlags) + tile;
+    uint32_t fl = 0;
+#pragma unroll 1
+    for (uint32_t s = 0; s < a.nFrames; ++s) fl |= (uint32_t)((w[(size_t)s * a.nTiles] >> lane) & 1ull) << s;
+    return fl;
+}
 __device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gid, uint32_t flags, float krad) {
     FrameRad f;
 #pragma unroll
@@ -1866,13 +1878,39 @@ __device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, FrameRad f)
 // The same chain with each frame's radiance loaded when its step runs: few registers, so the
 // accumulation waves fit beside a running render grid (RT_ACCUM_VGPRS, co-resident overlap;
 // rt_capi.cpp).  Same values, same operations, same order.
+// gamma_out with its six pow evaluated one after another (scheduling barriers between them): the
+// same operations and bits, at a third of the interleaved form's live registers
+template <class M>
+__device__ __forceinline__ F3 gamma_out_serial(uint32_t frameCount, F3 old, F3 rad) {
+    if (frameCount == 0) {
+        F3 o;
+        o.x = M::pow(rad.x, 0.45454545f);
+        __builtin_amdgcn_sched_barrier(0);
+        o.y = M::pow(rad.y, 0.45454545f);
+        __builtin_amdgcn_sched_barrier(0);
+        o.z = M::pow(rad.z, 0.45454545f);
+        return o;
+    }
+    const float fm1 = (float)(frameCount - 1), fc = (float)frameCount;
+    float c[3] = {old.x, old.y, old.z};
+    const float r[3] = {rad.x, rad.y, rad.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float lin = M::pow(c[i], 2.2f);
+        __builtin_amdgcn_sched_barrier(0);
+        c[i] = M::pow(M::div(madd<M>(lin, fm1, r[i]), fc), 0.454545f);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return F3{c[0], c[1], c[2]};
+}
+
 template <class M>
 __device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32_t gid, uint32_t flags, float krad) {
 #pragma unroll 1
     for (uint32_t s = 0; s < a.nFrames; ++s) {
         const float4 r = ((flags >> s) & 1u) ? make_float4(krad, krad, krad, 0.0f)
                                              : rad_load(a.radBuf + (size_t)s * a.radStride + gid);
-        v = gamma_out<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
+        v = gamma_out_serial<M>(a.frameCount + s, v, F3{r.x, r.y, r.z});
     }
     return v;
 }
@@ -1919,6 +1957,8 @@ constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels
 template <class M>
 __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uint32_t* key) {
     if (RT_ACCUM_PRIO > 0) __builtin_amdgcn_s_setprio(RT_ACCUM_PRIO);
+    // per wave: queued pixels as {tile of the wave t << 16 | frame flags << 8 | lane in the tile}
+    // (the chain needs the pixel's work-item id and its flags: both re-formed from one word)
     __shared__ uint32_t queue[kAccumWgWaves][kAccumQueue];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t* q = queue[wv];
@@ -1935,9 +1975,11 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         const bool live = x < a.width && row < a.rowBegin + a.rowCount && g64 >= a.gidBegin && g64 < a.gidEnd;
         const uint32_t gid = (uint32_t)g64;
         bool sky = false;
+        uint32_t fl = 0;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (live) {
-            const float4 o = a.frameCount != 0u ? a.result[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const uint32_t fl = load_flags(a, gid);
+            if (a.frameCount != 0u) o = a.result[gid];
+            fl = a.flagTiles ? load_tile_flags(a, tile, lane) : load_flags(a, gid);
             sky = fl == (1u << a.nFrames) - 1u &&
                   (a.frameCount == 0u ||
                    (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold));
@@ -1947,20 +1989,36 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
             }
         }
         const bool push = live && !sky;
+        if (kAccumTilesPerWave == 1u) {
+            // one tile per wave: the non-sky pixels accumulate in place (a queue would only move
+            // them to the low lanes of the same single round)
+            if (push) {
+#if RT_ACCUM_VGPRS
+                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, gid, fl, krf);
+#else
+                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, gid, fl, krf));
+#endif
+                a.result[gid] = make_float4(v.x, v.y, v.z, 0.0f);
+            }
+            continue;
+        }
         const unsigned long long m = __ballot(push);
-        if (push) q[qn + lane_rank(m)] = gid;
+        if (push) q[qn + lane_rank(m)] = t << 16 | fl << 8 | lane;
         qn += (uint32_t)__popcll(m);
         const bool last = t + 1 == kAccumTilesPerWave || tile + 1 >= a.nTiles;
         // accumulate up to 64 queued pixels, one per lane; after the wave's last tile, until empty
         // (one call site: the chain is the bulk of the kernel's code)
         while (qn >= 64u || (last && qn > 0u)) {
             if (lane < qn) {
-                const uint32_t g = q[lane];
+                const uint32_t e = q[lane], pl = e & 63u, gfl = (e >> 8) & 0xffu;
+                const uint32_t qt = tile0 + (e >> 16), qy = qt / a.tilesX;
+                const uint32_t g = (a.rowBegin + (qy * a.bandPeriod + a.bandPhase) * 8u + (pl >> 3)) * a.width +
+                                   (qt - qy * a.tilesX) * 8u + (pl & 7u);
                 const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #if RT_ACCUM_VGPRS
-                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, g, load_flags(a, g), krf);
+                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, g, gfl, krf);
 #else
-                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, load_flags(a, g), krf));
+                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, gfl, krf));
 #endif
                 a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
             }
