@@ -75,7 +75,7 @@ def parse():
                    help="host: the reference's SAH build (default); device: rtBuildBVH linear BVH")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
-    p.add_argument("--sched", choices=["regen", "tiles", "step", "pool", "wavefront"], default="step",
+    p.add_argument("--sched", choices=["tiles", "step", "wavefront"], default="step",
                    help="step (default): per-wave state machine in one persistent launch; wavefront: "
                         "extend + shade launches per bounce over HBM ray queues (SURVEY 8(f.3))")
     p.add_argument("--launch", choices=["fused", "per-frame"], default="fused",
@@ -155,8 +155,7 @@ def make_kernel(ctx, bufs, out, args):
     k.set_float3(N.CAMERA_FRONT, CAMERA[1])
     k.set_float3(N.CAMERA_UP, CAMERA[2])
     k.set_math_mode({"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[args.math])
-    k.set_schedule({"tiles": N.SCHED_TILES, "regen": N.SCHED_REGEN, "step": N.SCHED_STEP,
-                    "pool": N.SCHED_POOL, "wavefront": N.SCHED_WAVEFRONT}[args.sched])
+    k.set_schedule({"tiles": N.SCHED_TILES, "step": N.SCHED_STEP, "wavefront": N.SCHED_WAVEFRONT}[args.sched])
     for t in args.tune:
         name, value = t.split("=", 1)
         k.set_tuning(name, int(value))

@@ -126,15 +126,11 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem mem, int blocking, size_t offset
 int rtKernelSetMathMode(rt_kernel k, int mode);
 
 /* Work schedule of the kernel (same results, different lane scheduling):
- * RT_SCHED_REGEN           -- persistent lanes; a lane whose path ends starts the next
- *                             pixel of its wave's 8x8 chunk (path regeneration);
- * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles);
+ * RT_SCHED_TILES           -- one pixel per lane for all of its bounces (16x16 tiles): the
+ *                             reference's own shape (one work-item per pixel);
  * RT_SCHED_STEP (default)  -- per-wave state machine: every step advances each lane by one
  *                             BVH node or one triangle; shading and pixel refill run when
  *                             enough lanes are ready;
- * RT_SCHED_POOL            -- step traversal, plus a per-wave LDS pool of 64 path records:
- *                             lanes park finished traversals and keep tracing; shading runs
- *                             64 records at a time;
  * RT_SCHED_WAVEFRONT       -- wavefront path tracing: per bounce an extend
  *                             launch (traversal only, persistent waves pulling rays from an
  *                             HBM ray queue) and a shade launch (one lane per queued path,
@@ -143,10 +139,10 @@ int rtKernelSetMathMode(rt_kernel k, int mode);
  *                             rtEnqueueKernel too.  Queues take 72 B per work-item and frame.
  *                             lightBounces outside 1..64 run the step schedule. */
 #define RT_SCHED_TILES 0
-#define RT_SCHED_REGEN 1
 #define RT_SCHED_STEP 2
-#define RT_SCHED_POOL 3
 #define RT_SCHED_WAVEFRONT 4
+/* (1 and 3 -- path regeneration and a per-wave LDS path pool -- were measured slower than
+ * RT_SCHED_STEP and retired in round 3: rtKernelSetSchedule returns RT_INVALID_VALUE) */
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
 /* Device-side BVH build (extension): a linear BVH (Morton codes, radix
@@ -260,7 +256,6 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     wave >= 2.5 tail chunks)
  *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)
  *   TOP_NODES                         global path: top-of-tree nodes staged in LDS (0-1024, 384)
- *   POOL_SHADE / PARK_MIN / LOW_WORK  pool schedule thresholds (64 / 16 / 32)
  *   TILE_MAJOR                        fused work order: -1 auto (default), 0 frame-major, 1 tile-major
  *   PERFRAME_SKY                      per-frame sky shortcut: 0 off, 1 large launches (default),
  *                                     2 always
@@ -297,9 +292,7 @@ enum rt_tuning {
     RT_TUNE_TAIL_CHUNK = 7,
     RT_TUNE_BULK_PERCENT = 8,
     RT_TUNE_TOP_NODES = 9,
-    RT_TUNE_POOL_SHADE = 10,
-    RT_TUNE_PARK_MIN = 11,
-    RT_TUNE_LOW_WORK = 12,
+    /* 10-12: the retired pool schedule's thresholds (RT_INVALID_VALUE) */
     RT_TUNE_TILE_MAJOR = 13,
     RT_TUNE_PERFRAME_SKY = 14,
     RT_TUNE_WF_REFILL_MIN = 15,

@@ -70,11 +70,11 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB, MATH_SHIPPED = 0, 1, 2
-SCHED_TILES, SCHED_REGEN, SCHED_STEP, SCHED_POOL, SCHED_WAVEFRONT = 0, 1, 2, 3, 4
+SCHED_TILES, SCHED_STEP, SCHED_WAVEFRONT = 0, 2, 4  # (1, 3: retired schedules)
 # rt_tuning (rt_hip.h): scheduling parameters, results unchanged
 TUNING = {"refill_min": 0, "shade_min": 1, "refill_min_global": 2, "shade_min_global": 3,
           "step_weight_node": 4, "step_weight_leaf": 5, "chunk_pixels": 6, "tail_chunk": 7,
-          "bulk_percent": 8, "top_nodes": 9, "pool_shade": 10, "park_min": 11, "low_work": 12,
+          "bulk_percent": 8, "top_nodes": 9,
           "tile_major": 13, "perframe_sky": 14, "wf_refill_min": 15, "wf_streams_per_cu": 16,
           "wf_top_nodes": 17, "global_oct": 18, "perframe_defer": 19, "max_blocks": 20,
           "perframe_defer_min": 21}

@@ -63,7 +63,6 @@ struct rt_kernel_s {
     // profiles/r02/goct_sweep.txt)
     uint32_t refill_min_g = 0, shade_min_g = 0;
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
-    uint32_t pool_shade = 64, park_min = 16, low_work = 32;  // pool schedule thresholds
     // pixels per work-counter fetch: bulk, and the cap of the launch-sized tail chunk (swept on
     // MI355X: profiles/r02/chunk_sweep.txt; 128 / 64 of round 1 left the counter at its atomic
     // throughput once sky tiles were decided at ring fill: 4K Cornell 1.01 -> 0.79 ms/frame)
@@ -833,9 +832,6 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.shadeMin = k->shade_min;
     a.stepWeightNode = k->w_node;
     a.stepWeightLeaf = k->w_leaf;
-    a.poolShadeMin = k->pool_shade;
-    a.parkMin = k->park_min;
-    a.lowWork = k->low_work;
     a.nFrames = n_frames;
     a.radStride = (uint32_t)g1;
     a.radBuf = nullptr;
@@ -911,7 +907,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     const size_t smem =
         wf ? (lds ? ((size_t)a.octRecords + 3 * (size_t)k->n_tris) * 16 : (size_t)a.nTop * 64) +
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
-           : (lds ? scene_bytes : (size_t)a.nTop * 64) + (si == RT_SCHED_POOL ? 4 * rtk::kPoolWaveBytes : 0) +
+           : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
                  (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
                  (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
@@ -1166,7 +1162,7 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
 
 int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (!k) return RT_INVALID_KERNEL;
-    if (sched != RT_SCHED_TILES && sched != RT_SCHED_REGEN && sched != RT_SCHED_STEP && sched != RT_SCHED_POOL &&
+    if (sched != RT_SCHED_TILES && sched != RT_SCHED_STEP &&
         sched != RT_SCHED_WAVEFRONT)
         return RT_INVALID_VALUE;
     k->sched = sched;
@@ -1385,9 +1381,6 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
             break;
         case RT_TUNE_BULK_PERCENT: if (!in(0, 100)) return RT_INVALID_VALUE; k->bulk_percent = (uint32_t)value; break;
         case RT_TUNE_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->top_limit = (uint32_t)value; k->packed_nodes_gen = ~0ull; break;
-        case RT_TUNE_POOL_SHADE: if (!in(1, 64)) return RT_INVALID_VALUE; k->pool_shade = (uint32_t)value; break;
-        case RT_TUNE_PARK_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->park_min = (uint32_t)value; break;
-        case RT_TUNE_LOW_WORK: if (!in(1, 128)) return RT_INVALID_VALUE; k->low_work = (uint32_t)value; break;
         case RT_TUNE_TILE_MAJOR: if (!in(-1, 1)) return RT_INVALID_VALUE; k->tile_major = value; break;
         case RT_TUNE_MAX_BLOCKS: if (!in(0, 64)) return RT_INVALID_VALUE; k->max_blocks = value; break;
         case RT_TUNE_PERFRAME_SKY: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_sky = value; break;
@@ -1416,9 +1409,6 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_TAIL_CHUNK: *value = (int)k->tail_chunk; break;
         case RT_TUNE_BULK_PERCENT: *value = (int)k->bulk_percent; break;
         case RT_TUNE_TOP_NODES: *value = (int)k->top_limit; break;
-        case RT_TUNE_POOL_SHADE: *value = (int)k->pool_shade; break;
-        case RT_TUNE_PARK_MIN: *value = (int)k->park_min; break;
-        case RT_TUNE_LOW_WORK: *value = (int)k->low_work; break;
         case RT_TUNE_TILE_MAJOR: *value = k->tile_major; break;
         case RT_TUNE_MAX_BLOCKS: *value = k->max_blocks; break;
         case RT_TUNE_PERFRAME_SKY: *value = k->pf_sky; break;

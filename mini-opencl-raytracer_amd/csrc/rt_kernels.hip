@@ -36,25 +36,6 @@ __global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinn
     step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct>(a);
 }
 
-#ifdef RT_POOL_DEVICELIB_WAVES
-#define RT_POOL_DEVICELIB_OCC __attribute__((amdgpu_waves_per_eu(RT_POOL_DEVICELIB_WAVES, 8)))
-#else
-#define RT_POOL_DEVICELIB_OCC
-#endif
-#ifdef RT_POOL_PINNED_WAVES
-#define RT_POOL_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_POOL_PINNED_WAVES, 8)))
-#else
-#define RT_POOL_PINNED_OCC
-#endif
-template <bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) RT_POOL_DEVICELIB_OCC void kernel_entry_pool_devicelib(KernelArgs a) {
-    pool_body<MathDeviceLib, kLdsScene, kStats>(a);
-}
-template <bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) RT_POOL_PINNED_OCC void kernel_entry_pool_pinned(KernelArgs a) {
-    pool_body<MathPinned, kLdsScene, kStats>(a);
-}
-
 
 // ---- scene packing (runs once per bound scene) -----------------------------------------------
 __global__ void pack_shade(const rt_cl_triangle* __restrict__ in, float4* __restrict__ out, uint32_t n) {
@@ -101,11 +82,7 @@ static KernelFn pick_sched(int sched, bool bofs, bool goct) {
         if (!L) return goct ? kernel_entry_step_pinned<true, S, false, true> : kernel_entry_step_pinned<false, S, false>;
         return bofs ? kernel_entry_step_pinned<true, S, true> : kernel_entry_step_pinned<true, S, false>;
     }
-    if (sched == kSchedPool) {
-        if (M::kId == MathDeviceLib::kId) return kernel_entry_pool_devicelib<L, S>;
-        return kernel_entry_pool_pinned<L, S>;
-    }
-    return sched == kSchedRegen ? kernel_entry_regen<M, L, S> : kernel_entry<M, L, S>;
+    return kernel_entry<M, L, S>;
 }
 
 // bofs: LDS node records with the B planes at kOctB (KernelArgs::octB == kOctB); goct: a scene

@@ -38,7 +38,6 @@ struct KernelArgs {
     uint32_t refillMin, shadeMin;       // step schedule batching thresholds (lanes)
     uint32_t stepWeightNode, stepWeightLeaf;  // step schedule: relative cost of node / triangle steps
     uint32_t bandPeriod, bandPhase;     // 8-row bands: this launch renders bands b % period == phase
-    uint32_t poolShadeMin, parkMin, lowWork;  // pool schedule thresholds (records / lanes)
     // extensions
     int32_t* hitIds;                    // primary hit primitive per work-item (-1 = miss)
     float* hitT;                        // primary isect.t per work-item
@@ -60,9 +59,9 @@ struct KernelArgs {
 };
 
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
-constexpr int kSchedRegen = 1;  // persistent lanes with path regeneration
+// (1: path regeneration and 3: a per-wave LDS path pool were measured slower than the step
+// schedule and retired in round 3; DESIGN.md section 5 keeps their numbers)
 constexpr int kSchedStep = 2;   // per-wave state machine: node / triangle steps, batched shading
-constexpr int kSchedPool = 3;   // step traversal + per-wave LDS path pool, full-wave shading
 constexpr int kSchedWavefront = 4;  // extend / shade launches per bounce over HBM ray queues
 constexpr int kNumSched = 5;
 // frames per fused launch (rtEnqueueKernelFrames splits longer runs)
@@ -83,8 +82,6 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 #define RT_STEAL 1
 #endif
 constexpr uint32_t kStealBytes = RT_STEAL ? 4u * 8u + 32u : 0u;  // (padded to whole float4s)
-// pool schedule LDS per wave: 64 slots x 7 float4 + three 64-entry slot stacks
-constexpr uint32_t kPoolWaveBytes = 64u * 7u * 16u + 3u * 64u * 4u;
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address

@@ -642,106 +642,6 @@ __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, 
     return true;
 }
 
-// ---- path-regeneration schedule -------------------------------------------------------------
-// Same per-pixel computation, different scheduling: every lane of a persistent wave carries
-// one path; when a path ends (miss, pdf break, or lightBounces reached) the lane writes its
-// pixel and immediately starts the next pixel, taken from the wave's current 64-pixel chunk
-// (one 8x8 tile; one global atomic per chunk).  Lanes therefore stay busy across bounces
-// instead of idling until the longest path of their tile ends.  Every pixel still runs the
-// reference's exact sequence of operations with its own seed, so results are identical.
-template <class M, bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) void kernel_entry_regen(KernelArgs a) {
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;  // index space: 8x8-pixel tiles, tile-major
-    const uint32_t rowEnd = a.rowBegin + a.rowCount;
-    const int lane = tid & 63;
-
-    LaneStats st;
-    bool active = false;
-    uint32_t gid = 0, seed = 0, bounce = 0;
-    int32_t pid = -1;
-    float pt = 0.0f;
-    Ray ray{};
-    F3 radiance = f3s(0.0f), beta = f3s(1.0f);
-    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
-    // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
-    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
-    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
-    bool exhausted = false;                    // wave-uniform
-
-    for (;;) {
-        // ---- refill idle lanes from the wave's chunk --------------------------------------
-        while (!exhausted) {
-            const unsigned long long idle = __ballot(!active);
-            if (idle == 0ull) break;
-            if (chunk_used >= chunk_len) {
-                if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                    exhausted = true;
-                    break;
-                }
-                chunk_used = 0;
-            }
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
-            if (!active && rank < take) {
-                const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                const uint32_t x = tx * 8u + (w & 7u),
-                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
-                const uint64_t g64 = (uint64_t)row * a.width + x;
-                if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
-                    gid = (uint32_t)g64;
-                    seed = gid + fh;  // kernel_bvh.cl:445
-                    ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, seed);
-                    radiance = f3s(0.0f);
-                    beta = f3s(1.0f);
-                    bounce = 0;
-                    pid = -1;
-                    pt = 0.0f;
-                    if (bounces > 0u) {
-                        active = true;
-                    } else {
-                        finish_pixel<M>(a, gid, f3s(0.0f), pid, pt);  // no bounce: radiance 0
-                    }
-                }
-            }
-            chunk_used += take;
-        }
-        if (__ballot(active) == 0ull) {
-            if (exhausted) break;
-            continue;
-        }
-        // ---- one bounce of every live path -------------------------------------------------
-        if (active) {
-            if (kStats) ++st.rays;
-            const Traversal h = intersect<M, kLdsScene, kStats>(sc, a, ray, st.visits, st.tests);
-            if (bounce == 0u) {
-                pid = h.prim;
-                pt = h.t;
-            }
-            bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
-            ++bounce;
-            if (!more || bounce >= bounces) {
-                const F3 rad{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
-                finish_pixel<M>(a, gid, rad, pid, pt);
-                active = false;
-            }
-        }
-    }
-    if (kStats) flush_stats(a, st, lane);
-}
-
 // ---- step schedule: a per-wave state machine ------------------------------------------------
 // Every lane is in one of four states:
 //   IDLE  -- no path; refilled (new pixel -> camera ray) when enough lanes are idle
@@ -1411,413 +1311,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     }
 }
 
-// ---- pool schedule: per-wave LDS path pool, full-wave shading ------------------------------
-// The step schedule leaves a third of a wave idle during traversal at 9 bounces: lanes whose
-// traversal ended wait (up to the shading threshold) and freed lanes wait for a refill
-// batch (profiles/r01/phase_*.txt).  Here every wave owns a pool of 64 path records in LDS
-// (the "hit" or "continuation" of a path, 112 B slots) and three slot stacks:
-//   trace-ready -- a continuation ray produced by shading, waiting for a lane
-//   shade-ready -- a finished traversal (ray + {t, primitive, u, v}) waiting for shading
-//   free
-// A lane whose traversal ends parks its path as shade-ready -- exchanging it for a
-// continuation when one is waiting -- and keeps tracing; idle lanes take continuations, then
-// new camera rays.  Shading runs when 64 records are ready (a full wave), each lane
-// shading one record in registers separate from its own traversal state, and writes the
-// continuation back into the same slot (or accumulates the pixel when the path ends).
-// Per path the operations, their order and the RNG stream are the reference's, so every
-// pixel and hit is bit-identical to the other schedules.  No cross-wave communication:
-// the pool is wave-private, LDS ops of one wave execute in order, no barriers.
-constexpr uint32_t kFin = 3;  // pool schedule: traversal finished, waiting to be parked
-constexpr uint32_t kPoolSlots = 64;
-constexpr uint32_t kPoolChunks = 7;
-static_assert(kPoolWaveBytes == kPoolSlots * kPoolChunks * 16 + 3 * kPoolSlots * 4, "pool layout");
-
-struct PoolView {
-    float4* rec;       // [chunk][slot] float4
-    uint32_t* tstack;  // trace-ready slots
-    uint32_t* sstack;  // shade-ready slots
-    uint32_t* fstack;  // free slots
-};
-
-struct PathState {
-    uint32_t gid, seed, bounce;
-    F3 radiance, beta;
-};
-
-// shade-ready record: o, d, {t, prim, u, v}, path state
-__device__ __forceinline__ void pool_put_hit(const PoolView& p, uint32_t s, const Ray& r, const Traversal& h,
-                                             const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, h.t, __int_as_float(h.prim));
-    p.rec[2 * kPoolSlots + s] = make_float4(h.u, h.v, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
-    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
-    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_hit(const PoolView& p, uint32_t s, Ray& r, Traversal& h, PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    h = Traversal{c1.z, __float_as_int(c1.w), c2.x, c2.y};
-    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
-                   F3{c4.x, c4.y, c4.z}};
-}
-
-// trace-ready record: the initialised next ray (o, d, 1/d) and path state
-__device__ __forceinline__ void pool_put_ray(const PoolView& p, uint32_t s, const Ray& r, const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
-    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, 0.0f, __uint_as_float(ps.gid), __uint_as_float(ps.seed));
-    p.rec[3 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, __uint_as_float(ps.bounce));
-    p.rec[4 * kPoolSlots + s] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_ray(const PoolView& p, uint32_t s, Ray& r, PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    r.inv = F3{c1.z, c1.w, c2.x};
-    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
-    ps = PathState{__float_as_uint(c2.z), __float_as_uint(c2.w), __float_as_uint(c3.w), F3{c3.x, c3.y, c3.z},
-                   F3{c4.x, c4.y, c4.z}};
-}
-
-// a lane's in-flight state (any lane state), parked in a slot during a shading round
-__device__ __forceinline__ void pool_put_lane(const PoolView& p, uint32_t s, uint32_t state, const Ray& r,
-                                              const Traversal& h, uint32_t cur, uint32_t leaf_i,
-                                              uint32_t leaf_end, const PathState& ps) {
-    p.rec[0 * kPoolSlots + s] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    p.rec[1 * kPoolSlots + s] = make_float4(r.d.y, r.d.z, r.inv.x, r.inv.y);
-    p.rec[2 * kPoolSlots + s] = make_float4(r.inv.z, h.t, __int_as_float(h.prim), h.u);
-    p.rec[3 * kPoolSlots + s] = make_float4(h.v, __uint_as_float(cur), __uint_as_float(leaf_i),
-                                            __uint_as_float(leaf_end));
-    p.rec[4 * kPoolSlots + s] = make_float4(__uint_as_float(state), __uint_as_float(ps.gid),
-                                            __uint_as_float(ps.seed), __uint_as_float(ps.bounce));
-    p.rec[5 * kPoolSlots + s] = make_float4(ps.radiance.x, ps.radiance.y, ps.radiance.z, ps.beta.x);
-    p.rec[6 * kPoolSlots + s] = make_float4(ps.beta.y, ps.beta.z, 0.0f, 0.0f);
-}
-
-__device__ __forceinline__ void pool_get_lane(const PoolView& p, uint32_t s, uint32_t& state, Ray& r,
-                                              Traversal& h, uint32_t& cur, uint32_t& leaf_i, uint32_t& leaf_end,
-                                              PathState& ps) {
-    const float4 c0 = p.rec[0 * kPoolSlots + s], c1 = p.rec[1 * kPoolSlots + s], c2 = p.rec[2 * kPoolSlots + s],
-                 c3 = p.rec[3 * kPoolSlots + s], c4 = p.rec[4 * kPoolSlots + s], c5 = p.rec[5 * kPoolSlots + s],
-                 c6 = p.rec[6 * kPoolSlots + s];
-    r.o = F3{c0.x, c0.y, c0.z};
-    r.d = F3{c0.w, c1.x, c1.y};
-    r.inv = F3{c1.z, c1.w, c2.x};
-    r.sgn = (r.inv.x < 0.0f ? 1u : 0u) | (r.inv.y < 0.0f ? 2u : 0u) | (r.inv.z < 0.0f ? 4u : 0u);
-    h = Traversal{c2.y, __float_as_int(c2.z), c2.w, c3.x};
-    cur = __float_as_uint(c3.y);
-    leaf_i = __float_as_uint(c3.z);
-    leaf_end = __float_as_uint(c3.w);
-    state = __float_as_uint(c4.x);
-    ps = PathState{__float_as_uint(c4.y), __float_as_uint(c4.z), __float_as_uint(c4.w), F3{c5.x, c5.y, c5.z},
-                   F3{c5.w, c6.x, c6.y}};
-}
-
-template <class M, bool kLdsScene, bool kStats>
-__device__ __forceinline__ void pool_body(const KernelArgs& a) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    const int tid = threadIdx.x;
-    const SceneView sc = stage_scene<kLdsScene>(a);
-    const uint32_t scene_f4 = lds_scene_f4<kLdsScene>(a);
-    float4* region = smem + scene_f4 + (uint32_t)(tid >> 6) * (kPoolWaveBytes / 16u);
-    uint32_t* stacks = reinterpret_cast<uint32_t*>(region + kPoolChunks * kPoolSlots);
-    const PoolView pv{region, stacks, stacks + kPoolSlots, stacks + 2 * kPoolSlots};
-
-    const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
-    const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
-    const F3 camUp{a.camUp[0], a.camUp[1], a.camUp[2]};
-    const float angle = M::tan(0.5f * (45.0f * 3.1415f / 180.0f));  // kernel_bvh.cl:392
-    const uint32_t fh = frame_hash(a.frameCount);
-    const uint32_t bounces = (uint32_t)a.lightBounces;
-    const uint32_t total = a.nTiles * 64u;
-    const uint32_t rowEnd = a.rowBegin + a.rowCount;
-    const uint32_t lane = (uint32_t)(tid & 63);
-    const uint32_t kRefillMin = a.refillMin;  // camera rays when this many lanes are idle
-    const uint32_t kShadeMin = a.poolShadeMin;  // shade when this many records are ready
-    const uint32_t kParkMin = a.parkMin;      // park when this many traversals have ended
-    const uint32_t kLowWork = a.lowWork;      // ... or shade early when tracing work runs low
-
-    pv.fstack[lane] = lane;
-    uint32_t nt = 0, ns = 0, ne = kPoolSlots;  // stack depths (wave-uniform)
-
-    LaneStats st;
-    uint32_t state = kIdle;
-    PathState ps{0u, 0u, 0u, f3s(0.0f), f3s(1.0f)};
-    Ray ray{};
-    Traversal h{kMaxDist, -1, 0.0f, 0.0f};
-    uint32_t cur = 0, leaf_i = 0, leaf_end = 0;
-    // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
-    // one returning atomic per chunk, so the counter stays far from its throughput limit
-    uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
-    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
-    bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
-    bool exhausted = false;                    // wave-uniform
-    uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
-    const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
-    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
-             u_rrounds = 0, u_rlanes = 0, u_other = 0, u_finw = 0, u_idlew = 0, u_parks = 0;
-
-    for (;;) {
-        uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        // ---- park ended traversals: exchange for a continuation, else take a free slot -----
-        {
-            const unsigned long long fin = __ballot(state == kFin);
-            if (fin) {
-                const uint32_t nf = (uint32_t)__popcll(fin);
-                const uint32_t x = min(nf, nt), y = min(nf - x, ne);
-                if (kStats) u_parks += x + y;
-                if (state == kFin) {
-                    const uint32_t rank = lane_rank(fin);
-                    if (rank < x) {
-                        const uint32_t slot = pv.tstack[nt - 1u - rank];
-                        Ray nr;
-                        PathState nps;
-                        pool_get_ray(pv, slot, nr, nps);
-                        pool_put_hit(pv, slot, ray, h, ps);
-                        pv.sstack[ns + rank] = slot;
-                        ray = nr;
-                        ps = nps;
-                        state = kTrav;
-                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                        cur = 0;
-                    } else if (rank < x + y) {
-                        const uint32_t slot = pv.fstack[ne - 1u - (rank - x)];
-                        pool_put_hit(pv, slot, ray, h, ps);
-                        pv.sstack[ns + rank] = slot;
-                        state = kIdle;
-                    }
-                }
-                nt -= x;
-                ne -= y;
-                ns += x + y;
-            }
-        }
-        // ---- idle lanes take waiting continuations --------------------------------------------
-        {
-            const unsigned long long idle = __ballot(state == kIdle);
-            if (idle != 0ull && nt > 0u) {
-                const uint32_t x = min((uint32_t)__popcll(idle), nt);
-                if (state == kIdle) {
-                    const uint32_t rank = lane_rank(idle);
-                    if (rank < x) {
-                        const uint32_t slot = pv.tstack[nt - 1u - rank];
-                        pool_get_ray(pv, slot, ray, ps);
-                        pv.fstack[ne + rank] = slot;
-                        state = kTrav;
-                        h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                        cur = 0;
-                    }
-                }
-                nt -= x;
-                ne += x;
-            }
-        }
-        // ---- new pixels (camera rays) for idle lanes -------------------------------------------
-        {
-            const uint32_t n_idle = popc_ballot(state == kIdle);
-            const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
-            if (!exhausted && n_idle > 0u && (n_idle >= kRefillMin || n_act == 0u)) {
-                if (kStats) {
-                    ++u_rrounds;
-                    u_rlanes += n_idle;
-                }
-                while (!exhausted) {
-                    const unsigned long long idle = __ballot(state == kIdle);
-                    if (idle == 0ull) break;
-                    if (chunk_used >= chunk_len) {
-                        if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                            exhausted = true;
-                            break;
-                        }
-                        chunk_used = 0;
-                    }
-                    const uint32_t rank = lane_rank(idle);
-                    const uint32_t take = min((uint32_t)__popcll(idle), 64u - (chunk_used & 63u));  // within one 8x8 tile
-                    if (state == kIdle && rank < take) {
-                        const uint32_t w = (chunk_used & 63u) + rank;  // chunks are whole 8x8 tiles
-                        const uint32_t tile = (chunk_base + chunk_used) >> 6;  // wave-uniform (scalar division)
-                        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                        const uint32_t x = tx * 8u + (w & 7u),
-                                       row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
-                        const uint64_t g64 = (uint64_t)row * a.width + x;
-                        if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
-                            ps.gid = (uint32_t)g64;
-                            ps.seed = ps.gid + fh;  // kernel_bvh.cl:445
-                            ray = create_ray<M>(x, row, a.width, a.height, camPos, camFront, camUp, angle, ps.seed);
-                            ps.radiance = f3s(0.0f);
-                            ps.beta = f3s(1.0f);
-                            ps.bounce = 0;
-                            if (bounces > 0u) {
-                                state = kTrav;
-                                h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                                cur = 0;
-                                if (kStats) ++st.rays;
-                            } else {
-                                finish_pixel<M>(a, ps.gid, f3s(0.0f), -1, 0.0f);  // no bounce: radiance 0
-                            }
-                        }
-                    }
-                    chunk_used += take;
-                }
-            }
-        }
-        uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats) cyc_refill += tB - tA;
-        // ---- shading: one record per lane, a full wave when the pool is full ------------------
-        // Only with no continuation waiting (nt == 0): then every lane owns a slot for the
-        // round -- its shade-ready record's, or a free one -- and parks its own in-flight state
-        // there while it shades, so the traversal registers are free for the shading code.
-        const uint32_t n_act = popc_ballot(state == kTrav || state == kLeaf);
-        if (nt == 0u && (ns >= kShadeMin || (ns > 0u && n_act < kLowWork))) {
-            const uint32_t nb = ns;  // <= 64; ne == 64 - nb
-            if (kStats) {
-                ++u_srounds;
-                u_slanes += nb;
-            }
-            const bool mine = lane < nb;
-            const uint32_t slot = mine ? pv.sstack[nb - 1u - lane] : pv.fstack[ne - 1u - (lane - nb)];
-            Ray sr;
-            Traversal sh;
-            PathState sp;
-            // Every lane runs the shading code (a lane without a record shades a miss and
-            // discards it): no divergent region around the large shading body, which keeps
-            // the register allocation of this loop close to the step schedule's.
-            pool_get_hit(pv, slot, sr, sh, sp);
-            if (!mine) sh.prim = -1;
-            pool_put_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
-            // compiler-only fences: keep the spill and the reload real (no store-to-load
-            // forwarding of the parked state across the shading code)
-            __asm__ volatile("" ::: "memory");
-            if (mine && sp.bounce == 0u && a.hitIds) {
-                a.hitIds[sp.gid] = sh.prim;
-                a.hitT[sp.gid] = sh.t;
-            }
-            LaneStats sst;
-            const bool more = shade_bounce<M, kStats>(with_uv<M>(sc, sh, sr), sr, sp.radiance, sp.beta, sp.seed, sc,
-                                                      a, sst);
-            if (kStats && mine) st.hits += sst.hits;
-            ++sp.bounce;
-            const bool cont = mine && more && sp.bounce < bounces;
-            if (mine && !cont) {
-                finish_color<M>(a, sp.gid, F3{M::max(sp.radiance.x, 0.0f), M::max(sp.radiance.y, 0.0f),
-                                              M::max(sp.radiance.z, 0.0f)});
-            }
-            if (kStats && cont) ++st.rays;
-            __asm__ volatile("" ::: "memory");
-            pool_get_lane(pv, slot, state, ray, h, cur, leaf_i, leaf_end, ps);
-            const unsigned long long cm = __ballot(cont);
-            const unsigned long long fm = __ballot(mine && !cont);
-            if (cont) {
-                pool_put_ray(pv, slot, sr, sp);
-                pv.tstack[lane_rank(cm)] = slot;
-            } else if (mine) {
-                pv.fstack[ne + lane_rank(fm)] = slot;
-            }
-            nt = (uint32_t)__popcll(cm);
-            ne += (uint32_t)__popcll(fm);
-            ns = 0;
-            if (kStats) cyc_shade += __builtin_amdgcn_s_memtime() - tB;
-        }
-        if (n_act == 0u) {
-            if (exhausted && ns == 0u && nt == 0u && __ballot(state == kFin) == 0ull) break;
-            continue;
-        }
-
-        // ---- traversal steps (as in the step schedule) ----------------------------------------
-        for (;;) {
-            const uint32_t n_trav = popc_ballot(state == kTrav);
-            const uint32_t n_leaf = popc_ballot(state == kLeaf);
-            const uint32_t n_fin = popc_ballot(state == kFin);
-            if (n_trav + n_leaf == 0u) break;
-            if (n_fin >= kParkMin) break;
-            const uint32_t n_idle = 64u - n_trav - n_leaf - n_fin;
-            if (n_idle >= kRefillMin && (nt > 0u || !exhausted)) break;
-            if (nt == 0u && ns > 0u && n_trav + n_leaf < kLowWork) break;
-            const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
-            if (kStats) {
-                u_finw += n_fin;
-                u_idlew += n_idle;
-                u_other += leaf_step ? n_trav : n_leaf;
-                if (leaf_step) {
-                    ++u_tsteps;
-                    u_tlanes += n_leaf;
-                } else {
-                    ++u_nsteps;
-                    u_nlanes += n_trav;
-                }
-            }
-            constexpr int kNodeBurst = kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
-            constexpr int kTriBurst = kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
-            if (!leaf_step) {
-#pragma unroll
-                for (int rep = 0; rep < kNodeBurst; ++rep) {
-                    if (state == kTrav) {
-                        if (kStats) ++st.visits;
-                        uint32_t next, first = 0, count = 0;
-                        if (kLdsScene) {
-                            uint32_t code;
-                            if (oct_visit(sc, a, cur, ray, h.t, next, code)) {
-                                state = kLeaf;
-                                leaf_i = code;
-                            }
-                        } else if (node_visit<false>(sc, a, cur, ray, h.t, next, first, count)) {
-                            state = kLeaf;
-                            leaf_i = first;
-                            leaf_end = first + count;
-                        }
-                        cur = next;
-                        if (state == kTrav && next == (kLdsScene ? a.nNodes : kEnd)) state = kFin;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int rep = 0; rep < kTriBurst; ++rep) {
-                    if (state == kLeaf) {
-                        if (kStats) ++st.tests;
-                        if (kLdsScene) {
-                            const uint32_t idx = leaf_i & 0x00ffffffu;
-                            ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            if ((leaf_i >> 24) == 1u) state = cur == a.nNodes ? kFin : kTrav;
-                            leaf_i += 1u - kLeafMin;
-                        } else {
-                            ray_triangle<M, false>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
-                            ++leaf_i;
-                            if (leaf_i == leaf_end) state = cur == kEnd ? kFin : kTrav;
-                        }
-                    }
-                }
-            }
-        }
-        if (kStats) cyc_trav += __builtin_amdgcn_s_memtime() - tB;
-    }
-    if (kStats) {
-        flush_stats(a, st, (int)lane);
-        if (lane == 0) {
-            atomicAdd(&a.stats[4], (unsigned long long)cyc_refill);
-            atomicAdd(&a.stats[5], (unsigned long long)cyc_trav);
-            atomicAdd(&a.stats[6], (unsigned long long)cyc_shade);
-            atomicAdd(&a.stats[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
-            atomicAdd(&a.stats[8], (unsigned long long)u_nsteps);
-            atomicAdd(&a.stats[9], (unsigned long long)u_nlanes);
-            atomicAdd(&a.stats[10], (unsigned long long)u_tsteps);
-            atomicAdd(&a.stats[11], (unsigned long long)u_tlanes);
-            atomicAdd(&a.stats[12], (unsigned long long)u_srounds);
-            atomicAdd(&a.stats[13], (unsigned long long)u_slanes);
-            atomicAdd(&a.stats[14], (unsigned long long)u_rrounds);
-            atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);
-            atomicAdd(&a.stats[16], (unsigned long long)u_other);
-            atomicAdd(&a.stats[17], (unsigned long long)u_finw);
-            atomicAdd(&a.stats[18], (unsigned long long)u_idlew);
-            atomicAdd(&a.stats[19], (unsigned long long)u_parks);
-        }
-    }
-}
-
 // rtEnqueueKernelFrames: the gamma accumulation (kernel_bvh.cl:449-455) of frames
 // frameCount .. frameCount + nFrames - 1 in order, per pixel, from the radiances the fused step
 // launch left in radBuf[slot][gid].  Same pixel set as the step launch (8x8 tiles of the rank's
@@ -1827,8 +1320,8 @@ __device__ __forceinline__ void pool_body(const KernelArgs& a) {
 // + 0, 0) in every component of every frame (kernel_bvh.cl:358-362, :383); if it also held
 // K_old, its result is one per-launch constant K_out = chain(K_old; K_rad x nFrames), computed
 // once by accum_key (one lane, same policy and operations).  Those pixels are written
-// directly; the others go through a per-wave LDS queue and are accumulated 64 at a time, so
-// the 6 pow per pixel and frame run on full waves of non-sky pixels only.  The key never
+// directly; the others are accumulated in place (one 8x8 tile per wave), or -- several tiles
+// per wave (RT_ACCUM_TPW) -- through a per-wave LDS queue 64 at a time.  The key never
 // affects results, only how often the shortcut applies: K_old chains from the previous
 // launch's K_out (the value all-sky pixels then hold).
 // Key words: [0] valid, [1] K_rad bits, [2] K_old, [3] K_out.

@@ -30,10 +30,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOC
 void kernel_entry_step_shipped_goct(KernelArgs a) {
     step_body<MathShipped, true, kStats, false, true>(a);
 }
-template <bool kLdsScene, bool kStats>
-__global__ __launch_bounds__(256) void kernel_entry_pool_shipped(KernelArgs a) {
-    pool_body<MathShipped, kLdsScene, kStats>(a);
-}
 
 __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,8 +43,7 @@ static KernelFn pick_sched_shipped(int sched, bool bofs, bool goct) {
         if (!L) return goct ? kernel_entry_step_shipped_goct<S> : kernel_entry_step_shipped_global<S>;
         return bofs ? kernel_entry_step_shipped_lds<S, true> : kernel_entry_step_shipped_lds<S, false>;
     }
-    if (sched == kSchedPool) return kernel_entry_pool_shipped<L, S>;
-    return sched == kSchedRegen ? kernel_entry_regen<MathShipped, L, S> : kernel_entry<MathShipped, L, S>;
+    return kernel_entry<MathShipped, L, S>;
 }
 
 KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct) {

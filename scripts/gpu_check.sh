@@ -36,7 +36,6 @@ for step in "$@"; do
     benchbunny) run bench_bunny 600 python bench.py --scene bunny --no-cpu-baseline --steps 3 ;;
     phase) run phase 300 python scripts/phase_profile.py ;;
     phasebunny) RT_PHASE_SCENE=bunny run phase_bunny 300 python scripts/phase_profile.py ;;
-    phasepool) run phase_pool 300 python scripts/phase_profile.py step pool ;;
     refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
     configs) run cfg3_default 600 python bench.py && \
              run cfg3_pinned 300 python bench.py --math pinned --no-cpu-baseline && \

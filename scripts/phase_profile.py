@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase wave-cycle shares of the step / pool schedules (stats variant, s_memtime).
-Usage: phase_profile.py [step|pool ...]"""
+"""Diagnostic: per-phase wave-cycle shares of the step schedule (stats variant, s_memtime).
+Usage: phase_profile.py [step]"""
 import os
 import sys
 
@@ -18,7 +18,7 @@ else:
     sc = clrt.scene.cornell()
 scheds = sys.argv[1:] or ["step"]
 for name in scheds:
-  sched = {"step": N.SCHED_STEP, "pool": N.SCHED_POOL}[name]
+  sched = {"step": N.SCHED_STEP}[name]
   maths = [{"pinned": N.MATH_PINNED, "devicelib": N.MATH_DEVICELIB, "shipped": N.MATH_SHIPPED}[m]
            for m in os.environ.get("RT_PHASE_MATH", "shipped,devicelib,pinned").split(",")]
   lbs = [int(x) for x in os.environ.get("RT_PHASE_LB", "1,9").split(",")]

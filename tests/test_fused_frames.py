@@ -86,7 +86,7 @@ def test_fused_bunny_proxy():
 
 def test_fused_other_schedules_launch_per_frame(cornell):
     W, H = 160, 96
-    _same(_render(cornell, W, H, 1, 3, True, sched=N.SCHED_REGEN), _render(cornell, W, H, 1, 3, False))
+    _same(_render(cornell, W, H, 1, 3, True, sched=N.SCHED_TILES), _render(cornell, W, H, 1, 3, False))
 
 
 def test_fused_sky_shortcut_chain(cornell):
