@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Sum rocprofv3 --pmc counters per kernel over all of its dispatches, plus the trace's total
-duration per kernel.  usage: pmc_sum.py DIR [--all]  (DIR from scripts/pmc_kernels.sh or
+duration per kernel.  usage: pmc_sum.py DIR [--all]  (DIR from scripts/profile.sh or
 scripts/pmc_variants.sh; --all: also kernels without SQ_INSTS_VALU)"""
 import csv
 import glob

@@ -1,7 +1,9 @@
 #!/bin/bash
-# Write-traffic / counter probe of library variants (mini-opencl-raytracer_amd/lib/variants) against
-# the main build: one rocprofv3 pass per counter group and variant, the render launch's sums per
-# dispatch printed by scripts/pmc_sum.py.  usage: scripts/pmc_variants.sh "COUNTERS;COUNTERS" [bench args]
+# Counter groups of one bench command on the main build and on every library variant
+# (mini-opencl-raytracer_amd/lib/variants, scripts/build_variant.sh; none = the main build only): one
+# rocprofv3 --pmc pass per group and library, per-kernel sums printed by scripts/pmc_sum.py.
+# usage: scripts/pmc_variants.sh "COUNTERS;COUNTERS;..." [bench args]
+# (round 3 folded the one-off counter scripts into this one; scripts/README.md lists the group sets)
 set -u
 GROUPS_=$1; shift
 export TMPDIR=/tmp
