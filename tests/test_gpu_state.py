@@ -79,3 +79,22 @@ def test_8k_frame_slice_matches_oracle(cornell, oracle_mod):
     r.close()
     want = rgb(_oracle_frame(oracle_mod, cornell, W, H, 2, first=lo, last=hi))[lo:hi]
     assert (got.view(np.uint32) == want.view(np.uint32)).all()
+
+
+def test_retired_schedules_and_tunings_are_refused(cornell):
+    """The path-regeneration (1) and LDS path-pool (3) schedules and the pool's three tunings
+    (10-12) were retired in round 3: the C ABI refuses them (CL_INVALID_VALUE) and the kernel keeps
+    its previous schedule, which still renders."""
+    r = HipRenderer(cornell, 64, 48)
+    for sched in (1, 3, 5, -1):
+        with pytest.raises(N.RTError) as e:
+            r.k.set_schedule(sched)
+        assert e.value.code == -30  # CL_INVALID_VALUE
+    lib = r.k._lib
+    for tid in (10, 11, 12):
+        assert lib.rtKernelSetTuning(r.k.handle, tid, 16) == -30
+    for sched in (N.SCHED_TILES, N.SCHED_STEP, N.SCHED_WAVEFRONT):
+        r.k.set_schedule(sched)
+    r.frame(1, light_bounces=2)
+    assert np.isfinite(r.result()).all()
+    r.close()
