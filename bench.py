@@ -71,8 +71,9 @@ def parse():
                    help="shipped (default): bit-exact with the reference as clBuildProgram builds it; "
                         "devicelib: ... with -ffp-contract=off -cl-fp32-correctly-rounded-divide-sqrt; "
                         "pinned: bit-exact with the CPU oracle")
-    p.add_argument("--bvh", choices=["host", "device"], default="host",
-                   help="host: the reference's SAH build (default); device: rtBuildBVH linear BVH")
+    p.add_argument("--bvh", choices=["host", "device", "device-lbvh"], default="host",
+                   help="host: the reference's SAH build (default); device: rtBuildBVH (PLOC); "
+                        "device-lbvh: rtBuildBVHEx linear BVH")
     p.add_argument("--scene", choices=["cornell", "bunny"], default="cornell",
                    help="bunny = the deterministic ~70k-triangle proxy (config 5)")
     p.add_argument("--sched", choices=["tiles", "step", "wavefront"], default="step",
@@ -313,14 +314,15 @@ def main():
         scene = clrt_proxy.bunny_proxy()
     else:
         scene = clrt.scene.cornell()
-    if args.bvh == "device":  # linear BVH built on the GPU (rtBuildBVH)
+    if args.bvh.startswith("device"):  # BVH built on the GPU (rtBuildBVHEx)
         if args.scene == "bunny":
             raw = clrt.scene.load_obj(os.path.join(clrt_proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
             ft, fm = raw.triangles, raw.materials
         else:
             z = np.load(clrt.scene.CORNELL_NPZ, allow_pickle=False)
             ft, fm = z["triangles"].view(N.TRIANGLE_DTYPE), z["materials"].view(N.MATERIAL_DTYPE)
-        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=local)
+        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=local,
+                                            method="lbvh" if args.bvh == "device-lbvh" else "ploc")
 
     comm = None
     if world > 1 or args.force_dist:

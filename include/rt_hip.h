@@ -145,9 +145,11 @@ int rtKernelSetMathMode(rt_kernel k, int mode);
  * RT_SCHED_STEP and retired in round 3: rtKernelSetSchedule returns RT_INVALID_VALUE) */
 int rtKernelSetSchedule(rt_kernel k, int sched);
 
-/* Device-side BVH build (extension): a linear BVH (Morton codes, radix
- * tree) over the `n_tris` CLTriangle records of `tris` (file order), for meshes too large to
- * build on the host quickly.  Permutes `tris` in place into leaf order and writes the
+/* Device-side BVH build (extension) over the `n_tris` CLTriangle records of
+ * `tris` (file order), for meshes too large to build on the host quickly: the triangles sorted
+ * by Morton code, then clustered bottom-up (PLOC: mutual nearest neighbours by union surface
+ * area within a window of the sorted order -- SAH-like trees) or split by the radix tree of
+ * the codes (a linear BVH, cheaper to build and slower to render; rtBuildBVHEx).  Permutes `tris` in place into leaf order and writes the
  * depth-first CLLinearBVHNode[] into `nodes` (capacity >= (2*n_tris - 1) * 48 bytes), count
  * in *n_nodes -- the node contract of CLBVHnode.cpp:161-183, so the buffers bind to
  * KernelEntry as they are (the tree is the first *n_nodes records; the rest of a 2n-1 buffer is
@@ -155,6 +157,11 @@ int rtKernelSetSchedule(rt_kernel k, int sched);
  * triangles tie). */
 int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, rt_mem nodes,
                size_t* n_nodes);
+/* The same with the tree's topology chosen: RT_BVH_PLOC (rtBuildBVH's) or RT_BVH_LBVH. */
+#define RT_BVH_LBVH 0
+#define RT_BVH_PLOC 1
+int rtBuildBVHEx(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, int method, rt_mem nodes,
+                 size_t* n_nodes);
 
 /* Restrict the next launches to work-items [first, last) (pixel-row tiles for
  * multi-GPU sharding); last = 0 means "to global_work_size".  Work-item ids, and

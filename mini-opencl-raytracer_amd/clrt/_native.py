@@ -71,6 +71,7 @@ CAMERA_POS, CAMERA_FRONT, CAMERA_UP = 11, 12, 13
 MEM_READ_WRITE, MEM_WRITE_ONLY, MEM_READ_ONLY, MEM_COPY_HOST_PTR = 1, 2, 4, 32
 MATH_PINNED, MATH_DEVICELIB, MATH_SHIPPED = 0, 1, 2
 SCHED_TILES, SCHED_STEP, SCHED_WAVEFRONT = 0, 2, 4  # (1, 3: retired schedules)
+BVH_LBVH, BVH_PLOC = 0, 1  # rtBuildBVHEx
 # rt_tuning (rt_hip.h): scheduling parameters, results unchanged
 TUNING = {"refill_min": 0, "shade_min": 1, "refill_min_global": 2, "shade_min_global": 3,
           "step_weight_node": 4, "step_weight_leaf": 5, "chunk_pixels": 6, "tail_chunk": 7,
@@ -130,6 +131,8 @@ _HIP_PROTOS = {
     "rtKernelGetSceneInLDS": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "rtKernelForceGlobalScene": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtBuildBVH": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint, _vp, ctypes.POINTER(ctypes.c_size_t)]),
+    "rtBuildBVHEx": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, _vp,
+                                    ctypes.POINTER(ctypes.c_size_t)]),
     "rtBufferGetDevicePointer": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "rtBufferGetSize": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_size_t)]),
     "rtContextGetStream": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),

@@ -42,12 +42,13 @@ class CLContext:
         check(self._lib.rtEnqueueWriteBuffer(self.handle, buffer.handle, int(blocking), 0, data.nbytes,
                                              data.ctypes.data), "Failed to write buffer")
 
-    def BuildBVH(self, tris: "Buffer", n_tris: int, max_prims_in_node: int, nodes: "Buffer") -> int:
-        """rtBuildBVH: device-side linear BVH over `tris` (permuted in place); returns the
-        node count written to `nodes`."""
+    def BuildBVH(self, tris: "Buffer", n_tris: int, max_prims_in_node: int, nodes: "Buffer",
+                 method: int = N.BVH_PLOC) -> int:
+        """rtBuildBVHEx: device-side BVH (PLOC, or the linear BVH) over `tris` (permuted in place);
+        returns the node count written to `nodes`."""
         n = ctypes.c_size_t()
-        check(self._lib.rtBuildBVH(self.handle, tris.handle, int(n_tris), int(max_prims_in_node), nodes.handle,
-                                   ctypes.byref(n)), "Failed to build BVH")
+        check(self._lib.rtBuildBVHEx(self.handle, tris.handle, int(n_tris), int(max_prims_in_node), int(method),
+                                     nodes.handle, ctypes.byref(n)), "Failed to build BVH")
         return int(n.value)
 
     def CopyToDevicePointer(self, buffer: "Buffer", offset: int, size: int, dst: int) -> None:

@@ -93,9 +93,9 @@ def build_bvh(triangles: np.ndarray, materials: np.ndarray, max_prims_in_node: i
 
 
 def build_bvh_device(triangles: np.ndarray, materials: np.ndarray, max_prims_in_node: int = 4,
-                     device: int = 0) -> Scene:
-    """Device-side BVH build (rtBuildBVH): same array contract as build_bvh,
-    a linear BVH instead of the reference's SAH tree.  Needs a GPU."""
+                     device: int = 0, method: str = "ploc") -> Scene:
+    """Device-side BVH build (rtBuildBVHEx): same array contract as build_bvh,
+    a PLOC ("ploc") or linear ("lbvh") BVH instead of the reference's SAH tree.  Needs a GPU."""
     from . import _native as N
     from .device import CLContext
     tris = np.ascontiguousarray(triangles, dtype=TRIANGLE_DTYPE)
@@ -104,7 +104,7 @@ def build_bvh_device(triangles: np.ndarray, materials: np.ndarray, max_prims_in_
     try:
         tb = ctx.create_buffer(N.MEM_READ_WRITE | N.MEM_COPY_HOST_PTR, tris.nbytes, tris)
         nb = ctx.create_buffer(N.MEM_READ_WRITE, max(1, 2 * n - 1) * NODE_DTYPE.itemsize)
-        count = ctx.BuildBVH(tb, n, max_prims_in_node, nb)
+        count = ctx.BuildBVH(tb, n, max_prims_in_node, nb, {"lbvh": N.BVH_LBVH, "ploc": N.BVH_PLOC}[method])
         out_t = np.empty_like(tris)
         out_n = np.empty(count, NODE_DTYPE)
         ctx.ReadBuffer(tb, out_t, blocking=True)

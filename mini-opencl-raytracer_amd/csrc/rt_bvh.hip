@@ -11,7 +11,10 @@
 // triangles tie (the Cornell OBJ holds every face twice): parity is per geometry, and a
 // render of the device-built tree is bit-exact with the oracle rendering the same arrays.
 //
-// Steps: centroid bounds (block reduction) -> 30-bit Morton codes -> rocPRIM radix sort
+// Two topologies over the same Morton order (rtBuildBVHEx): PLOC (default, below: SAH-like trees
+// by bottom-up clustering) or the linear BVH of Karras (2012).
+//
+// LBVH steps: centroid bounds (block reduction) -> 30-bit Morton codes -> rocPRIM radix sort
 // (stable: equal codes keep triangle order) -> Karras (2012) binary radix tree over the
 // sorted order, ties broken by position -> bottom-up bounds and output-subtree sizes
 // (atomic arrival counters) -> every subtree with <= maxPrims triangles becomes one leaf
@@ -21,6 +24,7 @@
 #include <stdint.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "../../include/rt_cl_types.h"
 #include "rt_bvh.hpp"
@@ -248,9 +252,196 @@ __global__ void gather_tris(const rt_cl_triangle* __restrict__ in, const uint32_
     if (i < n) out[i] = in[order[i]];
 }
 
+// ---- PLOC: parallel locally-ordered clustering (Meister & Bittner 2018) -----------------------
+// The same Morton order, but the tree is built bottom-up by merging clusters: every cluster finds
+// the neighbour within kPlocRadius positions whose union box has the least surface area, mutual
+// nearest neighbours merge (the lower position keeps the new cluster, in Morton order), the cluster
+// array is compacted, until one cluster is left.  SAH-like trees at a linear BVH's build cost.
+// Nodes 0 .. n-1 are the triangles (sorted positions), n .. 2n-2 the merges (allocated in merge
+// order; the output depends only on the topology, so it is deterministic).
+constexpr int kPlocRadius = 16;
+constexpr uint32_t kNoParent = 0xffffffffu;
+
+__device__ inline Box box_union(const Box& a, const Box& b) {
+    Box u;
+    for (int k = 0; k < 3; ++k) {
+        u.lo[k] = fminf(a.lo[k], b.lo[k]);
+        u.hi[k] = fmaxf(a.hi[k], b.hi[k]);
+    }
+    return u;
+}
+__device__ inline float box_area(const Box& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+__global__ void ploc_init(const rt_cl_triangle* __restrict__ tris, const uint32_t* __restrict__ order, uint32_t n,
+                          Box* __restrict__ box, uint32_t* __restrict__ cnt, uint32_t* __restrict__ parent,
+                          uint32_t* __restrict__ clus) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        box[i] = tri_box(tris[order[i]]);
+        cnt[i] = 1u;
+        clus[i] = i;
+    }
+    if (i < 2 * n - 1) parent[i] = kNoParent;
+}
+
+// nearest neighbour (least union surface area; ties: the lower position) of clusters [0, m)
+__global__ void ploc_nn(const uint32_t* __restrict__ clus, uint32_t m, const Box* __restrict__ box,
+                        uint32_t* __restrict__ nn) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const Box bi = box[clus[i]];
+    const uint32_t lo = i > (uint32_t)kPlocRadius ? i - kPlocRadius : 0u;
+    const uint32_t hi = min(m - 1u, i + (uint32_t)kPlocRadius);
+    float best = INFINITY;
+    uint32_t bj = i == 0u ? 1u : i - 1u;
+    for (uint32_t j = lo; j <= hi; ++j) {
+        if (j == i) continue;
+        const float c = box_area(box_union(bi, box[clus[j]]));
+        if (c < best) {
+            best = c;
+            bj = j;
+        }
+    }
+    nn[i] = bj;
+}
+
+// mutual nearest neighbours merge (force: pairs (0,1), (2,3), ... -- only after a round without a
+// merge, which the lowest-cost pair rules out unless costs tie pathologically)
+__global__ void ploc_merge(const uint32_t* __restrict__ clus, uint32_t m, const uint32_t* __restrict__ nn,
+                           uint32_t n, uint32_t force, Box* __restrict__ box, uint32_t* __restrict__ cnt,
+                           uint32_t* __restrict__ left, uint32_t* __restrict__ right, uint32_t* __restrict__ parent,
+                           uint32_t* __restrict__ counter, uint32_t* __restrict__ next, uint32_t* __restrict__ flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint32_t j = nn[i];
+    bool pair = nn[j] == i;
+    if (force) {
+        j = i ^ 1u;
+        pair = j < m;
+    }
+    if (pair && i > j) {
+        flag[i] = 0u;
+        return;
+    }
+    if (pair) {
+        const uint32_t k = atomicAdd(counter, 1u), id = n + k;
+        const uint32_t a = clus[i], b = clus[j];
+        left[k] = a;
+        right[k] = b;
+        parent[a] = id;
+        parent[b] = id;
+        box[id] = box_union(box[a], box[b]);
+        cnt[id] = cnt[a] + cnt[b];
+        next[i] = id;
+    } else {
+        next[i] = clus[i];
+    }
+    flag[i] = 1u;
+}
+
+__global__ void ploc_compact(uint32_t m, const uint32_t* __restrict__ next, const uint32_t* __restrict__ flag,
+                             const uint32_t* __restrict__ pos, uint32_t* __restrict__ clus_out,
+                             uint32_t* __restrict__ m_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    if (flag[i]) clus_out[pos[i]] = next[i];
+    if (i == m - 1u) *m_out = pos[i] + flag[i];
+}
+
+// the axis along which two boxes' centres lie furthest apart (the node's `axis`: the walk visits
+// the second child first when the ray points down that axis, kernel_bvh.cl:200-207)
+__device__ inline int child_axis(const Box& a, const Box& b) {
+    float d[3];
+    for (int k = 0; k < 3; ++k) d[k] = fabsf((b.lo[k] + b.hi[k]) - (a.lo[k] + a.hi[k]));
+    return (d[0] >= d[1] && d[0] >= d[2]) ? 0 : (d[1] >= d[2] ? 1 : 2);
+}
+
+// order every merge's children along that axis (first child = the lower one), as a split would
+__global__ void ploc_orient(uint32_t n, const Box* __restrict__ box, uint32_t* __restrict__ left,
+                            uint32_t* __restrict__ right) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k + 1 >= n) return;
+    const uint32_t a = left[k], b = right[k];
+    const int ax = child_axis(box[a], box[b]);
+    if (box[a].lo[ax] + box[a].hi[ax] > box[b].lo[ax] + box[b].hi[ax]) {
+        left[k] = b;
+        right[k] = a;
+    }
+}
+
+// output-subtree sizes bottom-up (a subtree of <= max_prims triangles is ONE output leaf)
+__global__ void ploc_sizes(uint32_t n, uint32_t max_prims, const uint32_t* __restrict__ left,
+                           const uint32_t* __restrict__ right, const uint32_t* __restrict__ parent,
+                           const uint32_t* __restrict__ cnt, uint32_t* __restrict__ arrivals,
+                           uint32_t* __restrict__ osize) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    osize[p] = 1u;
+    __threadfence();
+    uint32_t node = parent[p];
+    while (node != kNoParent) {
+        const uint32_t k = node - n;
+        if (atomicAdd(&arrivals[k], 1u) == 0u) return;  // the sibling subtree finishes this node
+        __threadfence();
+        osize[node] = cnt[node] <= max_prims ? 1u : 1u + osize[left[k]] + osize[right[k]];
+        __threadfence();
+        node = parent[node];
+    }
+}
+
+// every node: its depth-first index and first triangle (walk to the root); output nodes write
+// their record, triangle nodes write their triangle at its depth-first position
+__global__ void ploc_emit(uint32_t n, uint32_t max_prims, uint32_t root, const uint32_t* __restrict__ left,
+                          const uint32_t* __restrict__ right, const uint32_t* __restrict__ parent,
+                          const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ osize,
+                          const Box* __restrict__ box, const rt_cl_triangle* __restrict__ in,
+                          const uint32_t* __restrict__ order, rt_cl_triangle* __restrict__ tris_out,
+                          rt_cl_bvh_node* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n - 1) return;
+    uint32_t idx = 0, first = 0;
+    for (uint32_t c = t; c != root;) {
+        const uint32_t par = parent[c], k = par - n;
+        idx += 1u;
+        if (right[k] == c) {
+            idx += osize[left[k]];
+            first += cnt[left[k]];
+        }
+        c = par;
+    }
+    if (t < n) tris_out[first] = in[order[t]];
+    if (t != root && cnt[parent[t]] <= max_prims) return;  // inside an output leaf
+    rt_cl_bvh_node nd;
+    for (int k = 0; k < 9; ++k) nd.pad[k] = 0;
+    const Box b = box[t];
+    nd.bounds.pmin = rt_float3{b.lo[0], b.lo[1], b.lo[2], 0.0f};
+    nd.bounds.pmax = rt_float3{b.hi[0], b.hi[1], b.hi[2], 0.0f};
+    if (t < n || cnt[t] <= max_prims) {
+        nd.offset = first;
+        nd.nPrimitives = (uint16_t)cnt[t];
+        nd.axis = 0;
+    } else {
+        nd.offset = idx + 1u + osize[left[t - n]];
+        nd.nPrimitives = 0;
+        nd.axis = (uint8_t)child_axis(box[left[t - n]], box[right[t - n]]);
+    }
+    out[idx] = nd;
+}
+
 }  // namespace rtb
 
 namespace rtb {
+
+static size_t scan_bytes(uint32_t n) {
+    size_t b = 0;
+    if (rocprim::exclusive_scan((void*)nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                (size_t)(n ? n : 1), rocprim::plus<uint32_t>()) != hipSuccess)
+        return 0;
+    return b;
+}
 
 size_t scratch_bytes(uint32_t n) {
     const size_t nn = n ? n : 1;
@@ -259,14 +450,22 @@ size_t scratch_bytes(uint32_t n) {
                                   (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned int)nn, 0, 30) != hipSuccess)
         return 0;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return al(64 * 6 * sizeof(float)) + 4 * al(nn * 4) +              // partials, keys/vals in+out
-           6 * al(nn * 4) + al(nn * 4) +                               // tree arrays, arrivals
-           al(nn * sizeof(Box)) * 2 + al(nn * 4) +                     // boxes, osize
-           al(nn * sizeof(rt_cl_triangle)) + al(sort_bytes);          // triangle copy, sort temp
+    const size_t common = al(64 * 6 * sizeof(float)) + 4 * al(nn * 4) +  // partials, keys/vals in+out
+                          al(nn * sizeof(rt_cl_triangle)) + al(sort_bytes);  // triangle copy, sort temp
+    const size_t lbvh = 6 * al(nn * 4) + al(nn * 4) +                   // tree arrays, arrivals
+                        al(nn * sizeof(Box)) * 2 + al(nn * 4);          // boxes, osize
+    const size_t ploc = al(2 * nn * sizeof(Box)) + 3 * al(2 * nn * 4) +  // boxes, cnt, parent, osize
+                        3 * al(nn * 4) +                                 // left, right, arrivals
+                        7 * al(nn * 4) + al(16) + al(scan_bytes(n));     // clusters x2, nn, next, flag, pos, m
+    return common + (lbvh > ploc ? lbvh : ploc);
 }
 
+static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh_node* nodes,
+                             uint32_t* n_nodes, uint8_t* p, rt_cl_triangle* copy, const uint32_t* svals,
+                             hipStream_t st);
+
 hipError_t build(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh_node* nodes, uint32_t* n_nodes,
-                 void* scratch, hipStream_t st) {
+                 void* scratch, hipStream_t st, int method) {
     if (n == 0) return hipErrorInvalidValue;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     uint8_t* p = static_cast<uint8_t*>(scratch);
@@ -281,16 +480,6 @@ hipError_t build(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh
     uint32_t* vals = (uint32_t*)take(nn * 4);
     uint32_t* skeys = (uint32_t*)take(nn * 4);
     uint32_t* svals = (uint32_t*)take(nn * 4);
-    uint32_t* left = (uint32_t*)take(nn * 4);
-    uint32_t* right = (uint32_t*)take(nn * 4);
-    uint32_t* first = (uint32_t*)take(nn * 4);
-    uint32_t* last = (uint32_t*)take(nn * 4);
-    uint32_t* pint = (uint32_t*)take(nn * 4);
-    uint32_t* pleaf = (uint32_t*)take(nn * 4);
-    uint32_t* arrivals = (uint32_t*)take(nn * 4);
-    Box* lbox = (Box*)take(nn * sizeof(Box));
-    Box* ibox = (Box*)take(nn * sizeof(Box));
-    uint32_t* osize = (uint32_t*)take(nn * 4);
     rt_cl_triangle* copy = (rt_cl_triangle*)take(nn * sizeof(rt_cl_triangle));
     size_t sort_bytes = 0;
     hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, sort_bytes, keys, skeys, vals, svals, (unsigned int)n, 0,
@@ -304,6 +493,18 @@ hipError_t build(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh
     hipLaunchKernelGGL(morton_codes, dim3((n + 255) / 256), b256, 0, st, tris, n, part, parts, keys, vals);
     e = rocprim::radix_sort_pairs(sort_tmp, sort_bytes, keys, skeys, vals, svals, (unsigned int)n, 0, 30, st);
     if (e != hipSuccess) return e;
+    if (method == 1) return build_ploc(tris, n, max_prims, nodes, n_nodes, p, copy, svals, st);
+
+    uint32_t* left = (uint32_t*)take(nn * 4);
+    uint32_t* right = (uint32_t*)take(nn * 4);
+    uint32_t* first = (uint32_t*)take(nn * 4);
+    uint32_t* last = (uint32_t*)take(nn * 4);
+    uint32_t* pint = (uint32_t*)take(nn * 4);
+    uint32_t* pleaf = (uint32_t*)take(nn * 4);
+    uint32_t* arrivals = (uint32_t*)take(nn * 4);
+    Box* lbox = (Box*)take(nn * sizeof(Box));
+    Box* ibox = (Box*)take(nn * sizeof(Box));
+    uint32_t* osize = (uint32_t*)take(nn * 4);
     if (n > 1) {
         hipLaunchKernelGGL(radix_tree, dim3((n - 1 + 255) / 256), b256, 0, st, skeys, (int)n, left, right, first, last,
                            pint, pleaf);
@@ -325,6 +526,75 @@ hipError_t build(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh
     e = hipMemcpyAsync(copy, tris, nn * sizeof(rt_cl_triangle), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gather_tris, dim3((n + 255) / 256), b256, 0, st, copy, svals, n, tris);
+    *n_nodes = total;
+    return hipGetLastError();
+}
+
+// PLOC over the sorted order `svals` (scratch from `p` on); the triangles are gathered from `copy`
+static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prims, rt_cl_bvh_node* nodes,
+                             uint32_t* n_nodes, uint8_t* p, rt_cl_triangle* copy, const uint32_t* svals,
+                             hipStream_t st) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    auto take = [&](size_t b) {
+        void* r = p;
+        p += al(b);
+        return r;
+    };
+    const size_t nn = n, n2 = 2 * nn;
+    Box* box = (Box*)take(n2 * sizeof(Box));
+    uint32_t* cnt = (uint32_t*)take(n2 * 4);
+    uint32_t* parent = (uint32_t*)take(n2 * 4);
+    uint32_t* osize = (uint32_t*)take(n2 * 4);
+    uint32_t* left = (uint32_t*)take(nn * 4);
+    uint32_t* right = (uint32_t*)take(nn * 4);
+    uint32_t* arrivals = (uint32_t*)take(nn * 4);
+    uint32_t* clus[2] = {(uint32_t*)take(nn * 4), (uint32_t*)take(nn * 4)};
+    uint32_t* nnb = (uint32_t*)take(nn * 4);
+    uint32_t* next = (uint32_t*)take(nn * 4);
+    uint32_t* flag = (uint32_t*)take(nn * 4);
+    uint32_t* pos = (uint32_t*)take(nn * 4);
+    uint32_t* dev = (uint32_t*)take(16);  // [0] merge counter, [1] cluster count
+    size_t sb = scan_bytes(n);
+    void* scan_tmp = take(sb);
+    const dim3 b256(256);
+    hipError_t e = hipMemsetAsync(dev, 0, 16, st);
+    if (e == hipSuccess) e = hipMemsetAsync(arrivals, 0, nn * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ploc_init, dim3((uint32_t)((n2 + 255) / 256)), b256, 0, st, tris, svals, n, box, cnt, parent,
+                       clus[0]);
+    // (`tris` is still in file order here; `copy` takes it before the emit permutes `tris`)
+    uint32_t m = n, cur = 0, force = 0;
+    while (m > 1) {
+        const dim3 g((m + 255) / 256);
+        hipLaunchKernelGGL(ploc_nn, g, b256, 0, st, clus[cur], m, box, nnb);
+        hipLaunchKernelGGL(ploc_merge, g, b256, 0, st, clus[cur], m, nnb, n, force, box, cnt, left, right, parent, dev,
+                           next, flag);
+        e = rocprim::exclusive_scan(scan_tmp, sb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(ploc_compact, g, b256, 0, st, m, next, flag, pos, clus[cur ^ 1], dev + 1);
+        uint32_t m_new = 0;
+        e = hipMemcpyAsync(&m_new, dev + 1, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        force = m_new == m;  // no mutual pair this round (ties): pair neighbours next round
+        if (m_new > m) return hipErrorUnknown;
+        m = m_new;
+        cur ^= 1;
+    }
+    uint32_t root = 0;
+    e = hipMemcpyAsync(&root, clus[cur], 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    if (n > 1) hipLaunchKernelGGL(ploc_orient, dim3((n - 1 + 255) / 256), b256, 0, st, n, box, left, right);
+    hipLaunchKernelGGL(ploc_sizes, dim3((n + 255) / 256), b256, 0, st, n, max_prims, left, right, parent, cnt, arrivals,
+                       osize);
+    uint32_t total = 1;
+    e = hipMemcpyAsync(&total, osize + root, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(copy, tris, nn * sizeof(rt_cl_triangle), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ploc_emit, dim3((uint32_t)((n2 - 1 + 255) / 256)), b256, 0, st, n, max_prims, root, left, right,
+                       parent, cnt, osize, box, copy, svals, tris, nodes);
     *n_nodes = total;
     return hipGetLastError();
 }

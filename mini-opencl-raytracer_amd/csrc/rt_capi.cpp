@@ -119,6 +119,9 @@ struct rt_kernel_s {
     uint64_t packed_tris_gen = ~0ull, packed_nodes_gen = ~0ull, checked_mats_gen = ~0ull;
     float4* packed_tris = nullptr;
     float4* oct_nodes = nullptr;       // [node][octant] 2 x float4 (LDS-resident scenes)
+    float4* goct_nodes = nullptr;      // regrouped octant records for the HBM/L2 walk (RT_GOCT_GROUP)
+    size_t goct_nodes_cap = 0;
+    uint32_t goct_b = 0;               // their B planes' float4 offset
     float4* shade_tris = nullptr;      // compact shading records (normals + mtlIndex)
     float4* shade_mats = nullptr;      // compact materials
     size_t shade_tris_cap = 0, shade_mats_cap = 0;
@@ -304,6 +307,38 @@ bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
     return ok;
 }
 
+#ifndef RT_GOCT_GROUP
+#define RT_GOCT_GROUP 1  // node-major: bunny proxy fused 1.405 -> 1.393 ms/frame (profiles/r03/goct_layout_ab.txt)
+#endif
+// The same octant records regrouped for the walk over HBM/L2 (RT_GOCT_GROUP = G > 0): blocks of G
+// consecutive nodes, each block laid out octant-major ([block][octant][G nodes], A planes then B
+// planes), so G = 1 puts the eight octants' records of a node in one 128-B line (lanes of different
+// octants at the same node -- every traversal starts at the root -- read one line, not eight) and
+// larger G keeps neighbouring nodes of one octant together as the octant-major layout does.  Links
+// are stored as walk words (block * 8G + node in block), so the kernel's index (octant x octStride
+// + word) holds with octStride = G; END = the sentinel's word.
+inline uint32_t goct_word(uint32_t i, uint32_t G) { return (i / G) * 8u * G + i % G; }
+void build_oct_nodes_grouped(const std::vector<uint32_t>& oct, uint32_t n, uint32_t G, std::vector<uint32_t>& out,
+                             uint32_t* b_ofs) {
+    const uint32_t stride = oct_stride(n), bofs = oct_b(n);
+    const uint32_t na = ((n + 1 + G - 1) / G) * 8u * G;  // A records, sentinel included, whole blocks
+    *b_ofs = na;
+    out.assign((size_t)2 * na * 4, 0u);
+    for (uint32_t i = 0; i <= n; ++i)
+        for (uint32_t o = 0; o < 8; ++o) {
+            const uint32_t* ra = &oct[((size_t)o * stride + i) * 4];
+            const uint32_t* rb = &oct[((size_t)bofs + (size_t)o * stride + i) * 4];
+            const size_t at = (size_t)goct_word(i, G) + (size_t)o * G;
+            uint32_t* wa = &out[at * 4];
+            uint32_t* wb = &out[((size_t)na + at) * 4];
+            for (int c = 0; c < 4; ++c) wa[c] = ra[c];
+            wb[0] = rb[0];
+            wb[1] = rb[1];
+            wb[2] = rb[2] >= kLeafMin ? rb[2] : goct_word(rb[2], G);  // leaf code as it is, else the near child
+            wb[3] = goct_word(rb[3], G);
+        }
+}
+
 template <class T>
 int ensure_dev(T*& p, size_t& cap, size_t count) {
     if (cap >= count) return RT_SUCCESS;
@@ -419,6 +454,17 @@ int prepare_scene(rt_kernel k) {
     {
         hipError_t e = hipMemcpyAsync(k->oct_nodes, oct.data(), oct.size() * sizeof(uint32_t),
                                       hipMemcpyHostToDevice, qs(k->ctx));
+        if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
+        if (e != hipSuccess) return map_hip(e);
+    }
+    k->goct_b = 0;
+    if (RT_GOCT_GROUP && oct_ok && (uint64_t)(nn + RT_GOCT_GROUP) * 8u < kLeafMin) {
+        std::vector<uint32_t> nm;
+        build_oct_nodes_grouped(oct, nn, RT_GOCT_GROUP, nm, &k->goct_b);
+        rc = ensure_dev(k->goct_nodes, k->goct_nodes_cap, nm.size() / 4);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(k->goct_nodes, nm.data(), nm.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                      qs(k->ctx));
         if (e == hipSuccess) e = hipStreamSynchronize(qs(k->ctx));
         if (e != hipSuccess) return map_hip(e);
     }
@@ -664,6 +710,7 @@ int rtReleaseKernel(rt_kernel k) {
     if (k->wf_cnt) (void)hipFree(k->wf_cnt);
     if (k->packed_tris) (void)hipFree(k->packed_tris);
     if (k->oct_nodes) (void)hipFree(k->oct_nodes);
+    if (k->goct_nodes) (void)hipFree(k->goct_nodes);
     if (k->g_nodes) (void)hipFree(k->g_nodes);
     if (k->shade_tris) (void)hipFree(k->shade_tris);
     if (k->shade_mats) (void)hipFree(k->shade_mats);
@@ -901,6 +948,14 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // (RT_TUNE_GLOBAL_OCT) instead of the 64-B global node records
     const bool goct = !lds && (wf || si == RT_SCHED_STEP) && k->oct_ok && k->global_oct;
     a.nTop = lds || goct ? 0u : k->n_top;  // global path: top-of-tree node records staged in LDS
+    if (goct && RT_GOCT_GROUP && k->goct_nodes && k->goct_b) {
+        // regrouped records, links as walk words (build_oct_nodes_grouped)
+        a.octNodes = k->goct_nodes;
+        a.octStride = RT_GOCT_GROUP;
+        a.octB = k->goct_b;
+        a.octRecords = 2u * a.octB;
+        a.nNodes = goct_word(k->n_nodes, RT_GOCT_GROUP);  // the END word
+    }
     a.refillMin = lds ? k->refill_min : k->refill_min_g ? k->refill_min_g : goct ? 16u : 8u;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g ? k->shade_min_g : 48u;
     if (wf) a.nTop = std::min(a.nTop, k->wf_top_limit);
@@ -1083,6 +1138,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
 int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, rt_mem nodes,
                size_t* n_nodes) {
+    return rtBuildBVHEx(ctx, tris, n_tris, max_prims_in_node, RT_BVH_PLOC, nodes, n_nodes);
+}
+
+int rtBuildBVHEx(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in_node, int method, rt_mem nodes,
+                 size_t* n_nodes) {
+    if (method != RT_BVH_LBVH && method != RT_BVH_PLOC) return RT_INVALID_VALUE;
     int rc = ensure_device(ctx);
     if (rc) return rc;
     if (!tris || !nodes || tris->ctx != ctx || nodes->ctx != ctx) return RT_INVALID_MEM_OBJECT;
@@ -1095,7 +1156,7 @@ int rtBuildBVH(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_in
     if (e != hipSuccess) return map_hip(e);
     uint32_t count = 0;
     e = rtb::build(static_cast<rt_cl_triangle*>(tris->dptr), (uint32_t)n_tris, mp,
-                   static_cast<rt_cl_bvh_node*>(nodes->dptr), &count, scratch, qs(ctx));
+                   static_cast<rt_cl_bvh_node*>(nodes->dptr), &count, scratch, qs(ctx), method);
     if (e == hipSuccess) e = hipStreamSynchronize(qs(ctx));
     (void)hipFree(scratch);
     if (e != hipSuccess) return map_hip(e);

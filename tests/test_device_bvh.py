@@ -32,10 +32,14 @@ def _same_multiset(a, b):
     return key(a) == key(b)
 
 
+METHODS = ["ploc", "lbvh"]
+
+
+@pytest.mark.parametrize("method", METHODS)
 @pytest.mark.parametrize("max_prims", [1, 2, 4, 8])
-def test_device_bvh_structure(max_prims):
+def test_device_bvh_structure(max_prims, method):
     tris, mats = _file_order_cornell()
-    sc = S.build_bvh_device(tris, mats, max_prims)
+    sc = S.build_bvh_device(tris, mats, max_prims, method=method)
     _check_bvh(sc)
     leaf = sc.nodes["nPrimitives"]
     assert leaf.max() <= max_prims
@@ -43,17 +47,19 @@ def test_device_bvh_structure(max_prims):
     assert _same_multiset(sc.triangles, tris)
 
 
+@pytest.mark.parametrize("method", METHODS)
 @pytest.mark.parametrize("n", [1, 3])
-def test_device_bvh_single_leaf(n):
+def test_device_bvh_single_leaf(n, method):
     tris, mats = _file_order_cornell()
-    sc = S.build_bvh_device(tris[:n], mats, 4)
+    sc = S.build_bvh_device(tris[:n], mats, 4, method=method)
     assert sc.nodes.shape[0] == 1 and sc.nodes[0]["nPrimitives"] == n
     _check_bvh(sc)
 
 
-def test_device_bvh_render_bit_exact_vs_oracle(oracle_mod):
+@pytest.mark.parametrize("method", METHODS)
+def test_device_bvh_render_bit_exact_vs_oracle(oracle_mod, method):
     tris, mats = _file_order_cornell()
-    sc = S.build_bvh_device(tris, mats, 4)
+    sc = S.build_bvh_device(tris, mats, 4, method=method)
     W, H = 160, 90
     r = HipRenderer(sc, W, H, stats=True)
     for f in (1, 2):
@@ -72,13 +78,14 @@ def test_device_bvh_render_bit_exact_vs_oracle(oracle_mod):
     assert (st["node_visits"], st["tri_tests"]) == (counts["node_visits"], counts["tri_tests"])
 
 
-def test_device_bvh_bunny_matches_sah_image():
+@pytest.mark.parametrize("method", METHODS)
+def test_device_bvh_bunny_matches_sah_image(method):
     """70k-triangle proxy: the device tree renders the same geometry as the SAH tree."""
     from clrt import proxy
     host = proxy.bunny_proxy()
     raw = S.load_obj(proxy.os.path.join(proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
     t0 = time.perf_counter()
-    dev = S.build_bvh_device(raw.triangles, raw.materials, 4)
+    dev = S.build_bvh_device(raw.triangles, raw.materials, 4, method=method)
     build_s = time.perf_counter() - t0
     _check_bvh(dev)
     assert _same_multiset(dev.triangles, host.triangles)
@@ -103,12 +110,13 @@ def test_device_bvh_bunny_matches_sah_image():
     rel = rel_err(a, b).max(axis=-1)
     assert (rel > 1e-4).mean() < 0.005               # radiance: last-bit differences from ties
     same = (a.view(np.uint32) == b.view(np.uint32)).all(axis=-1).mean()
-    print(f"device build of {raw.triangles.shape[0]} triangles: {build_s * 1e3:.1f} ms incl. transfers; "
+    print(f"device {method} build of {raw.triangles.shape[0]} triangles: {build_s * 1e3:.1f} ms incl. transfers; "
           f"same face {agree:.5f}; {same:.4f} of pixels bit-identical to the SAH tree's image")
 
 
+@pytest.mark.parametrize("method", [N.BVH_PLOC, N.BVH_LBVH])
 @pytest.mark.parametrize("max_prims", [1, 4])
-def test_device_bvh_buffers_bind_to_kernel_entry_as_they_are(oracle_mod, max_prims):
+def test_device_bvh_buffers_bind_to_kernel_entry_as_they_are(oracle_mod, max_prims, method):
     """rt_hip.h's flow for rtBuildBVH: the triangle and node buffers it wrote are bound to
     KernelEntry directly -- the node buffer keeps its 2n-1 records (the tree is the first
     `count`, the rest unused) -- and the render equals the oracle's on the tree read back."""
@@ -120,7 +128,7 @@ def test_device_bvh_buffers_bind_to_kernel_entry_as_they_are(oracle_mod, max_pri
     tb = ctx.create_buffer(N.MEM_READ_WRITE | N.MEM_COPY_HOST_PTR, tris.nbytes, tris)
     nb = ctx.create_buffer(N.MEM_READ_WRITE, (2 * n - 1) * N.NODE_DTYPE.itemsize)
     mb = ctx.create_buffer(N.MEM_READ_ONLY | N.MEM_COPY_HOST_PTR, mats.nbytes, mats)
-    count = ctx.BuildBVH(tb, n, max_prims, nb)
+    count = ctx.BuildBVH(tb, n, max_prims, nb, method)
     assert (max_prims == 1) == (count == 2 * n - 1)
     out = ctx.create_buffer(N.MEM_WRITE_ONLY, W * H * 16)
     k = clrt.CLKernel(ctx)
@@ -150,3 +158,26 @@ def test_device_bvh_buffers_bind_to_kernel_entry_as_they_are(oracle_mod, max_pri
     sc = S.Scene(t_dev, n_dev, mats, max_prims)
     want, _, _, _ = oracle_mod.render(sc, W, H, frame_count=1, light_bounces=4, threads=16)
     assert (rgb(got).view(np.uint32) == rgb(want).view(np.uint32)).all()
+
+
+def _sah_cost(sc):
+    """Surface-area-heuristic cost of a depth-first node array (interior 1, triangle test 1 per
+    triangle), relative to the root box: the expected work of a random ray that hits the root."""
+    lo, hi = sc.nodes["bmin"][:, :3].astype(np.float64), sc.nodes["bmax"][:, :3].astype(np.float64)
+    d = np.maximum(hi - lo, 0.0)
+    area = 2.0 * (d[:, 0] * d[:, 1] + d[:, 1] * d[:, 2] + d[:, 2] * d[:, 0])
+    cnt = sc.nodes["nPrimitives"].astype(np.float64)
+    return float(np.sum(area * np.where(cnt > 0, cnt, 1.0)) / area[0])
+
+
+def test_device_bvh_ploc_tree_beats_lbvh():
+    """PLOC clusters by surface area: on the 70k-triangle proxy its tree's SAH cost is well below
+    the linear BVH's and within reach of the host SAH build (the reference's algorithm)."""
+    from clrt import proxy
+    host = proxy.bunny_proxy()
+    raw = S.load_obj(proxy.os.path.join(proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
+    c = {m: _sah_cost(S.build_bvh_device(raw.triangles, raw.materials, 4, method=m)) for m in METHODS}
+    c["host_sah"] = _sah_cost(host)
+    print("SAH cost:", {k: round(v, 2) for k, v in c.items()})
+    assert c["ploc"] < 0.9 * c["lbvh"], c
+    assert c["ploc"] < 1.3 * c["host_sah"], c
