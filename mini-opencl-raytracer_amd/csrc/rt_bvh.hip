@@ -259,7 +259,10 @@ __global__ void gather_tris(const rt_cl_triangle* __restrict__ in, const uint32_
 // array is compacted, until one cluster is left.  SAH-like trees at a linear BVH's build cost.
 // Nodes 0 .. n-1 are the triangles (sorted positions), n .. 2n-2 the merges (allocated in merge
 // order; the output depends only on the topology, so it is deterministic).
-constexpr int kPlocRadius = 16;
+#ifndef RT_PLOC_RADIUS
+#define RT_PLOC_RADIUS 32
+#endif
+constexpr int kPlocRadius = RT_PLOC_RADIUS;
 constexpr uint32_t kNoParent = 0xffffffffu;
 
 __device__ inline Box box_union(const Box& a, const Box& b) {
@@ -372,21 +375,40 @@ __global__ void ploc_orient(uint32_t n, const Box* __restrict__ box, uint32_t* _
     }
 }
 
-// output-subtree sizes bottom-up (a subtree of <= max_prims triangles is ONE output leaf)
+// output-subtree sizes bottom-up; osize 1 = the node is an output leaf.  RT_PLOC_SAH_LEAVES 0: every
+// subtree of <= max_prims triangles is one leaf; 1: such a subtree becomes a leaf only where the
+// surface area heuristic prefers it, as the reference's SAH build decides (CLBVHnode.cpp, pbrt:
+// leaf cost = triangles, split cost = 1 + children's costs weighted by area), here on the
+// children's own (recursive) costs
+#ifndef RT_PLOC_SAH_LEAVES
+#define RT_PLOC_SAH_LEAVES 0
+#endif
 __global__ void ploc_sizes(uint32_t n, uint32_t max_prims, const uint32_t* __restrict__ left,
                            const uint32_t* __restrict__ right, const uint32_t* __restrict__ parent,
-                           const uint32_t* __restrict__ cnt, uint32_t* __restrict__ arrivals,
-                           uint32_t* __restrict__ osize) {
+                           const uint32_t* __restrict__ cnt, const Box* __restrict__ box, float* __restrict__ cost,
+                           uint32_t* __restrict__ arrivals, uint32_t* __restrict__ osize) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     osize[p] = 1u;
+    cost[p] = 1.0f;
     __threadfence();
     uint32_t node = parent[p];
     while (node != kNoParent) {
         const uint32_t k = node - n;
         if (atomicAdd(&arrivals[k], 1u) == 0u) return;  // the sibling subtree finishes this node
         __threadfence();
-        osize[node] = cnt[node] <= max_prims ? 1u : 1u + osize[left[k]] + osize[right[k]];
+        const uint32_t l = left[k], r = right[k];
+        bool leaf = cnt[node] <= max_prims;
+        float c = (float)cnt[node];
+        if (RT_PLOC_SAH_LEAVES) {
+            const float a = box_area(box[node]);
+            const float split = a > 0.0f ? 1.0f + (box_area(box[l]) * cost[l] + box_area(box[r]) * cost[r]) / a
+                                         : 1.0f + cost[l] + cost[r];
+            leaf = leaf && c <= split;
+            if (!leaf) c = split;
+        }
+        cost[node] = c;
+        osize[node] = leaf ? 1u : 1u + osize[l] + osize[r];
         __threadfence();
         node = parent[node];
     }
@@ -403,6 +425,7 @@ __global__ void ploc_emit(uint32_t n, uint32_t max_prims, uint32_t root, const u
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 2 * n - 1) return;
     uint32_t idx = 0, first = 0;
+    bool inside = false;  // below an output leaf
     for (uint32_t c = t; c != root;) {
         const uint32_t par = parent[c], k = par - n;
         idx += 1u;
@@ -410,16 +433,17 @@ __global__ void ploc_emit(uint32_t n, uint32_t max_prims, uint32_t root, const u
             idx += osize[left[k]];
             first += cnt[left[k]];
         }
+        inside = inside || osize[par] == 1u;
         c = par;
     }
     if (t < n) tris_out[first] = in[order[t]];
-    if (t != root && cnt[parent[t]] <= max_prims) return;  // inside an output leaf
+    if (inside) return;
     rt_cl_bvh_node nd;
     for (int k = 0; k < 9; ++k) nd.pad[k] = 0;
     const Box b = box[t];
     nd.bounds.pmin = rt_float3{b.lo[0], b.lo[1], b.lo[2], 0.0f};
     nd.bounds.pmax = rt_float3{b.hi[0], b.hi[1], b.hi[2], 0.0f};
-    if (t < n || cnt[t] <= max_prims) {
+    if (osize[t] == 1u) {
         nd.offset = first;
         nd.nPrimitives = (uint16_t)cnt[t];
         nd.axis = 0;
@@ -454,7 +478,7 @@ size_t scratch_bytes(uint32_t n) {
                           al(nn * sizeof(rt_cl_triangle)) + al(sort_bytes);  // triangle copy, sort temp
     const size_t lbvh = 6 * al(nn * 4) + al(nn * 4) +                   // tree arrays, arrivals
                         al(nn * sizeof(Box)) * 2 + al(nn * 4);          // boxes, osize
-    const size_t ploc = al(2 * nn * sizeof(Box)) + 3 * al(2 * nn * 4) +  // boxes, cnt, parent, osize
+    const size_t ploc = al(2 * nn * sizeof(Box)) + 4 * al(2 * nn * 4) +  // boxes, cnt, parent, osize, cost
                         3 * al(nn * 4) +                                 // left, right, arrivals
                         7 * al(nn * 4) + al(16) + al(scan_bytes(n));     // clusters x2, nn, next, flag, pos, m
     return common + (lbvh > ploc ? lbvh : ploc);
@@ -545,6 +569,7 @@ static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prim
     uint32_t* cnt = (uint32_t*)take(n2 * 4);
     uint32_t* parent = (uint32_t*)take(n2 * 4);
     uint32_t* osize = (uint32_t*)take(n2 * 4);
+    float* cost = (float*)take(n2 * 4);
     uint32_t* left = (uint32_t*)take(nn * 4);
     uint32_t* right = (uint32_t*)take(nn * 4);
     uint32_t* arrivals = (uint32_t*)take(nn * 4);
@@ -586,8 +611,8 @@ static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prim
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return e;
     if (n > 1) hipLaunchKernelGGL(ploc_orient, dim3((n - 1 + 255) / 256), b256, 0, st, n, box, left, right);
-    hipLaunchKernelGGL(ploc_sizes, dim3((n + 255) / 256), b256, 0, st, n, max_prims, left, right, parent, cnt, arrivals,
-                       osize);
+    hipLaunchKernelGGL(ploc_sizes, dim3((n + 255) / 256), b256, 0, st, n, max_prims, left, right, parent, cnt, box,
+                       cost, arrivals, osize);
     uint32_t total = 1;
     e = hipMemcpyAsync(&total, osize + root, 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(copy, tris, nn * sizeof(rt_cl_triangle), hipMemcpyDeviceToDevice, st);
