@@ -672,7 +672,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * RT_RAD_SETS);
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * (RT_RAD_SETS + 1));
+    if (e == hipSuccess) e = hipMemsetAsync(k->work_counter, 0, 16 * (RT_RAD_SETS + 1), qs(ctx));
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
     if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
@@ -872,7 +873,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     const uint64_t n_tiles = tilesY * a.tilesX;
     if (n_tiles * 64 > 0xfff00000ull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
-    a.workCounter = k->work_counter;
+    a.workCounter = k->work_counter + 4 * RT_RAD_SETS;  // per-frame launches: their own counters
     a.chunkPixels = k->chunk_pixels;
     a.tailChunk = k->tail_chunk;
     a.refillMin = k->refill_min;
@@ -1072,7 +1073,15 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         wa.refillMin = k->wf_refill_min;
         grid_s = G;  // one workgroup per stream
     }
-    if (si != RT_SCHED_TILES && !wf) {
+    // the chunk counters start at zero: per-frame launches clear theirs here; a fused render's
+    // (its radiance set's) were cleared by the accumulation that followed the set's previous render
+    // (accum_key_body), which this render already waits for -- no clearing launch in front of it
+#ifdef RT_DIAG_NO_ACCUM
+    const bool clear_here = true;  // (diagnostic builds without the accumulation launch)
+#else
+    const bool clear_here = !fused;
+#endif
+    if (si != RT_SCHED_TILES && !wf && clear_here) {
         hipError_t me = hipMemsetAsync(a.workCounter, 0, 16, rstr);
         if (me != hipSuccess) return map_hip(me);
     }

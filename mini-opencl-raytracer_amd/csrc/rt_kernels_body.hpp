@@ -1411,6 +1411,12 @@ __device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32
 template <class M>
 __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* key) {
     if (threadIdx.x != 0) return;
+    // the render this accumulation follows is done with its chunk counters: clear them for the
+    // radiance set's next render (rt_capi.cpp launches it after this accumulation)
+    if (a.workCounter) {
+        a.workCounter[0] = 0u;
+        a.workCounter[1] = 0u;
+    }
     const float krad = M::max(madd<M>(1.0f, 0.5f * a.skyboxIntensity, 0.0f), 0.0f);
     const float kold = key[0] == 1u ? __uint_as_float(key[3]) : 0.0f;
     F3 v = f3s(kold);
