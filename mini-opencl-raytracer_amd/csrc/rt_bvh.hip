@@ -311,8 +311,8 @@ __global__ void ploc_nn(const uint32_t* __restrict__ clus, uint32_t m, const Box
     nn[i] = bj;
 }
 
-// mutual nearest neighbours merge (force: pairs (0,1), (2,3), ... -- only after a round without a
-// merge, which the lowest-cost pair rules out unless costs tie pathologically)
+// mutual nearest neighbours merge (force: pairs (0,1), (2,3), ... -- only after a round that merged
+// (almost) nothing, which happens only where costs tie across the whole window)
 __global__ void ploc_merge(const uint32_t* __restrict__ clus, uint32_t m, const uint32_t* __restrict__ nn,
                            uint32_t n, uint32_t force, Box* __restrict__ box, uint32_t* __restrict__ cnt,
                            uint32_t* __restrict__ left, uint32_t* __restrict__ right, uint32_t* __restrict__ parent,
@@ -601,7 +601,9 @@ static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prim
         e = hipMemcpyAsync(&m_new, dev + 1, 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return e;
-        force = m_new == m;  // no mutual pair this round (ties): pair neighbours next round
+        // a round that merged almost nothing (costs that tie everywhere, e.g. copies of one
+        // triangle: every cluster picks the same lowest neighbour) -> pair neighbours next round
+        force = m_new == m || (m > 64u && (m - m_new) * 64u < m);
         if (m_new > m) return hipErrorUnknown;
         m = m_new;
         cur ^= 1;
