@@ -283,11 +283,20 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     (faster when the host synchronises every frame, as the
  *                                     reference's RenderFrame does, and for small frames);
  *                                     2 (default) = defer a launch of at least PERFRAME_DEFER_MIN
- *                                     work items exactly when the previous per-frame render of the
- *                                     kernel is still running (the host is queueing frames)
+ *                                     work items when the host has not waited on the context
+ *                                     through this API (rtFinish, a blocking read or write) since
+ *                                     the kernel's previous per-frame launch -- i.e. frames are
+ *                                     being queued.  A host that synchronises some other way
+ *                                     (hipStreamSynchronize on rtContextGetStream's stream,
+ *                                     hipDeviceSynchronize, events) looks like a queueing host to
+ *                                     this rule and should set 0.  Results never change.
  *   PERFRAME_DEFER_MIN                work items from which PERFRAME_DEFER 2 defers (default 4 Mi)
  *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
- *                                     as many as fit, default; fewer = fewer waves per SIMD) */
+ *                                     as many as fit, default; fewer = fewer waves per SIMD)
+ *   SPEC_WALK                         step schedule, octant walks: 1 (default) = speculative walk
+ *                                     (a lane walks on past a passed leaf while its triangles are
+ *                                     pending; same bits), 0 = the plain walk.  Trees whose child
+ *                                     boxes do not nest in their parents' always walk plainly. */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -308,7 +317,8 @@ enum rt_tuning {
     RT_TUNE_GLOBAL_OCT = 18,
     RT_TUNE_PERFRAME_DEFER = 19,
     RT_TUNE_MAX_BLOCKS = 20,
-    RT_TUNE_PERFRAME_DEFER_MIN = 21
+    RT_TUNE_PERFRAME_DEFER_MIN = 21,
+    RT_TUNE_SPEC_WALK = 22
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);
@@ -337,7 +347,7 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
  * pipelining and unpack as above, with the transfer step (grouped ncclSend/ncclRecv) replaced by
  * device copies into the root's receive slots on the root's communicator stream.  The contexts
  * may share one device (several ranks on one GPU), so the N > 1 gather runs where there is only
- * one GPU.  Every gather and reduction must pass all n communicators (n_local == n). */
+ * one GPU.  Every gather and reduction must pass all n communicators (n_local == n); n <= 64. */
 int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out);
 int rtCommDestroy(rt_comm comm);
 int rtCommGetRank(rt_comm comm, int* rank, int* nranks);
@@ -353,9 +363,10 @@ int rtCommShardKernel(rt_comm comm, rt_kernel k);
  * the context's accumulation stream), RCCL moves them (grouped send/recv: the root receives on
  * all links at once; its own bands go through RCCL too, a device-local send to itself, so a
  * world of one runs the same flow) on the communicator's stream and the root unpacks them on a
- * third stream,
- * so the next fused render is not held up; two staging slots, so step k's gather overlaps step
- * k+1's render.  Every later call on a context that reads or writes memory (rtFinish,
+ * third stream (gathering into its own `out`, the root's own bands are in place and not
+ * unpacked), so neither the next fused render nor the next accumulation is held up by the
+ * transfer; two staging slots, so step k's gather overlaps step k+1's render.  The
+ * communicator's streams run at the device's greatest stream priority.  Every later call on a context that reads or writes memory (rtFinish,
  * rtEnqueueReadBuffer, per-frame launches, ...) is ordered after the gather. */
 int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_local, unsigned width,
                              unsigned height, int root, rt_mem root_dst);

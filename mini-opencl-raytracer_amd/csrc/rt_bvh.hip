@@ -459,20 +459,22 @@ __global__ void ploc_emit(uint32_t n, uint32_t max_prims, uint32_t root, const u
 
 namespace rtb {
 
-static size_t scan_bytes(uint32_t n) {
-    size_t b = 0;
-    if (rocprim::exclusive_scan((void*)nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                (size_t)(n ? n : 1), rocprim::plus<uint32_t>()) != hipSuccess)
-        return 0;
-    return b;
+// rocPRIM's temporary-storage query for the PLOC compaction scan; false when the query fails
+static bool scan_bytes(uint32_t n, size_t& b) {
+    b = 0;
+    return rocprim::exclusive_scan((void*)nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                   (size_t)(n ? n : 1), rocprim::plus<uint32_t>()) == hipSuccess;
 }
 
+// Scratch bytes rtb::build needs for n triangles, or 0 when a rocPRIM size query fails (the caller
+// reports an error instead of building in an under-sized scratch).
 size_t scratch_bytes(uint32_t n) {
     const size_t nn = n ? n : 1;
-    size_t sort_bytes = 0;
+    size_t sort_bytes = 0, sb = 0;
     if (rocprim::radix_sort_pairs((void*)nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                   (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned int)nn, 0, 30) != hipSuccess)
         return 0;
+    if (!scan_bytes(n, sb)) return 0;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t common = al(64 * 6 * sizeof(float)) + 4 * al(nn * 4) +  // partials, keys/vals in+out
                           al(nn * sizeof(rt_cl_triangle)) + al(sort_bytes);  // triangle copy, sort temp
@@ -480,7 +482,7 @@ size_t scratch_bytes(uint32_t n) {
                         al(nn * sizeof(Box)) * 2 + al(nn * 4);          // boxes, osize
     const size_t ploc = al(2 * nn * sizeof(Box)) + 4 * al(2 * nn * 4) +  // boxes, cnt, parent, osize, cost
                         3 * al(nn * 4) +                                 // left, right, arrivals
-                        7 * al(nn * 4) + al(16) + al(scan_bytes(n));     // clusters x2, nn, next, flag, pos, m
+                        7 * al(nn * 4) + al(16) + al(sb);                // clusters x2, nn, next, flag, pos, m
     return common + (lbvh > ploc ? lbvh : ploc);
 }
 
@@ -579,7 +581,8 @@ static hipError_t build_ploc(rt_cl_triangle* tris, uint32_t n, uint32_t max_prim
     uint32_t* flag = (uint32_t*)take(nn * 4);
     uint32_t* pos = (uint32_t*)take(nn * 4);
     uint32_t* dev = (uint32_t*)take(16);  // [0] merge counter, [1] cluster count
-    size_t sb = scan_bytes(n);
+    size_t sb = 0;
+    if (!scan_bytes(n, sb)) return hipErrorInvalidValue;
     void* scan_tmp = take(sb);
     const dim3 b256(256);
     hipError_t e = hipMemsetAsync(dev, 0, 16, st);

@@ -126,6 +126,8 @@ struct rt_kernel_s {
     float4* shade_mats = nullptr;      // compact materials
     size_t shade_tris_cap = 0, shade_mats_cap = 0;
     bool oct_ok = false;               // every leaf fits the records' inline {first, count}
+    bool nested = false;               // every child box lies inside its parent's (speculative walk)
+    int spec_walk = 1;                 // RT_TUNE_SPEC_WALK
     float4* g_nodes = nullptr;         // global-scene node records (64 B, top of the tree first)
     size_t g_nodes_cap = 0;
     uint32_t n_top = 0, top_limit = 384;  // nodes of g_nodes staged in LDS (global path; swept, profiles/r01/bunny_top_nodes_sweep_2.txt)
@@ -201,6 +203,25 @@ int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* dept
     // The reference's 64-entry stack (kernel_bvh.cl:181) would overflow past depth 64; the
     // stackless walk here has no such limit, so deeper trees are rendered, not rejected.
     return RT_SUCCESS;
+}
+
+// The speculative walk (rt_kernels_body.hpp, step_body) needs every interior node's box to hold
+// its children's: then a child whose box a ray passes at some t has every ancestor passed at that
+// t too (the slab arithmetic is monotone in the planes and in t), which is what lets a lane walk
+// ahead of a pending leaf and re-test only the node it stops at.  The reference's builder forms
+// parents as unions of their children (CLBVHnode.cpp:7-159, CLmathlib.hpp:190-204), and so do
+// rtBuildBVH's; a hand-made tree that breaks it (or holds NaN planes) is walked plainly.
+bool boxes_nest(const rt_cl_bvh_node* nd, uint32_t n) {
+    auto inside = [](const rt_cl_bvh_node& c, const rt_cl_bvh_node& p) {
+        return c.bounds.pmin.x >= p.bounds.pmin.x && c.bounds.pmin.y >= p.bounds.pmin.y &&
+               c.bounds.pmin.z >= p.bounds.pmin.z && c.bounds.pmax.x <= p.bounds.pmax.x &&
+               c.bounds.pmax.y <= p.bounds.pmax.y && c.bounds.pmax.z <= p.bounds.pmax.z;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+        if (nd[i].nPrimitives > 0) continue;
+        if (!inside(nd[i + 1], nd[i]) || !inside(nd[nd[i].offset], nd[i])) return false;
+    }
+    return true;
 }
 
 // Per-octant skip pointers (see rt_kernels.hip, intersect): for octant o (bit i = the ray
@@ -490,6 +511,7 @@ int prepare_scene(rt_kernel k) {
     k->n_mats = nmat;
     k->depth = depth;
     k->oct_ok = oct_ok;
+    k->nested = boxes_nest(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn);
     k->n_top = n_top;
     k->packed_for_tris = tm;
     k->packed_tris_gen = tm->generation;
@@ -808,8 +830,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // A loop that synchronises every frame -- the reference's RenderFrame: ExecuteKernel,
     // ReadBuffer, Finish -- gains nothing from it and pays the second launch, and so do small
     // frames; frames queued back to back gain (4K Cornell 1.11 -> 0.92 ms/frame).  So by default
-    // (PERFRAME_DEFER 2) a large launch defers exactly when the previous per-frame render of this
-    // kernel has not finished yet: the host is queueing, not waiting
+    // (PERFRAME_DEFER 2) a large launch defers when the host has not waited on the context through
+    // this API since the kernel's previous per-frame launch: the host is queueing, not waiting
     // (profiles/r03/perframe_defer_auto.txt).  "Queueing" = no host wait on the context (rtFinish,
     // a blocking read or write) since the previous per-frame launch: no GPU-side query, which
     // would itself cost the read-back loop (an event after every render: 3.63 -> 4.07 ms/frame).
@@ -921,8 +943,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             // accumulation: it fills the CUs that render's draining waves free.  (With hit
             // buffers bound the renders stay in order on the main stream: each writes them.)
             rstr = ctx->rstream[rs];
-            hipError_t me = hipEventRecord(ctx->mtail, ctx->stream);
-            if (me == hipSuccess) me = hipStreamWaitEvent(rstr, ctx->mtail, 0);
+            hipError_t me = rti::main_tail_wait(ctx, rstr);
             if (me != hipSuccess) return map_hip(me);
         }
         // the render writes the set: after the accumulation that last read it
@@ -936,6 +957,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // one chunk counter per radiance set: renders of the two sets may run together
         a.workCounter = k->work_counter + 4 * rs;
     }
+    // everything below (counter clear, timing events, the render; the accumulation when it is not
+    // overlapped) goes to rstr: the main stream unless a render stream was taken above
+    if (rstr == ctx->stream) ctx->mdirty = true;
     a.hitIds = k->hit_ids ? static_cast<int32_t*>(k->hit_ids->dptr) : nullptr;
     a.hitT = k->hit_t ? static_cast<float*>(k->hit_t->dptr) : nullptr;
     a.stats = k->dstats;
@@ -971,6 +995,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end
     a.flagTiles = fused && !wf && si == RT_SCHED_STEP && lds && RT_RAY_RING ? 1u : 0u;
+    a.specWalk = k->spec_walk && k->nested ? 1u : 0u;
 
     const int mi = k->math;
     const bool bofs = lds && a.octB == rtk::kOctB;
@@ -1106,22 +1131,30 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // accumulation stream after this render, overlapping whatever the main stream runs next
         // (the next fused render uses the other radiance set); qs() joins it back
         hipStream_t as = ctx->stream;
+        if (!ctx->overlap) ctx->mdirty = true;
+        // The render left its chunk counters for this accumulation to clear (accum_key_body); if
+        // the accumulation cannot be enqueued, clear them behind the render (same stream as the
+        // set's next render), so that render does not start with spent counters and skip tiles.
+        auto fail = [&](int rc) {
+            (void)hipMemsetAsync(a.workCounter, 0, 16, rstr);
+            return rc;
+        };
         if (ctx->overlap) {
             as = ctx->astream;
             e = hipEventRecord(k->render_done, rstr);
             if (e == hipSuccess) e = hipStreamWaitEvent(as, k->render_done, 0);
-            if (e != hipSuccess) return map_hip(e);
+            if (e != hipSuccess) return fail(map_hip(e));
         }
         hipEvent_t ea = nullptr, eb = nullptr;
         if (k->timing) {
             ea = take_event(k);
             eb = take_event(k);
-            if (!ea || !eb) return RT_OUT_OF_RESOURCES;
+            if (!ea || !eb) return fail(RT_OUT_OF_RESOURCES);
             (void)hipEventRecord(ea, as);
         }
 #ifndef RT_DIAG_NO_ACCUM  // diagnostic A/B builds only (wrong images): the render without its accumulation
         e = rtk::launch_accum_frames(a, k->math, k->accum_key, as);
-        if (e != hipSuccess) return map_hip(e);
+        if (e != hipSuccess) return fail(map_hip(e));
 #endif
         if (k->timing) {
             (void)hipEventRecord(eb, as);
@@ -1161,7 +1194,9 @@ int rtBuildBVHEx(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_
     if (nodes->size < (2 * n_tris - 1) * sizeof(rt_cl_bvh_node)) return RT_INVALID_BUFFER_SIZE;
     const uint32_t mp = std::max(1u, std::min(max_prims_in_node, 65535u));
     void* scratch = nullptr;
-    hipError_t e = hipMalloc(&scratch, rtb::scratch_bytes((uint32_t)n_tris));
+    const size_t scratch_size = rtb::scratch_bytes((uint32_t)n_tris);
+    if (scratch_size == 0) return RT_OUT_OF_RESOURCES;  // rocPRIM could not size its temporaries
+    hipError_t e = hipMalloc(&scratch, scratch_size);
     if (e != hipSuccess) return map_hip(e);
     uint32_t count = 0;
     e = rtb::build(static_cast<rt_cl_triangle*>(tris->dptr), (uint32_t)n_tris, mp,
@@ -1276,8 +1311,10 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
         // `out` there; a fused render's tail is the accumulation's own dependency, so waiting on
         // it costs the overlap nothing); later main-stream work that joins (qs) waits for the
         // copy too
-        hipError_t e = hipEventRecord(ctx->mtail, ctx->stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->astream, ctx->mtail, 0);
+        hipError_t e = rti::main_tail_wait(ctx, ctx->astream);
+        // ... and after the gathers queued so far (their unpack writes a root's image; nothing
+        // else on astream waits for it)
+        if (e == hipSuccess && ctx->gpending) e = hipStreamWaitEvent(ctx->astream, ctx->gtail, 0);
         if (e == hipSuccess)
             e = hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
                                  width_bytes, rows, hipMemcpyDeviceToDevice, ctx->astream);
@@ -1299,6 +1336,7 @@ int rtContextSetReadbackOnAccumStream(rt_context ctx, int enable) {
 int rtContextGetAccumStream(rt_context ctx, void** s) {
     if (!ctx) return RT_INVALID_CONTEXT;
     if (!s) return RT_INVALID_VALUE;
+    if (!ctx->overlap) ctx->mexposed = true;  // the main stream leaves the library's view
     *s = ctx->overlap ? ctx->astream : qs(ctx);
     return RT_SUCCESS;
 }
@@ -1412,6 +1450,7 @@ int rtBufferGetSize(rt_mem m, size_t* size) {
 
 int rtContextGetStream(rt_context ctx, void** s) {
     if (!ctx || !s) return RT_INVALID_VALUE;
+    ctx->mexposed = true;  // the caller may enqueue there without going through the library
     *s = qs(ctx);
     return RT_SUCCESS;
 }
@@ -1460,6 +1499,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_GLOBAL_OCT: if (!in(0, 1)) return RT_INVALID_VALUE; k->global_oct = value; break;
         case RT_TUNE_PERFRAME_DEFER: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_defer = value; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: if (value < 0) return RT_INVALID_VALUE; k->pf_defer_min = (uint32_t)value; break;
+        case RT_TUNE_SPEC_WALK: if (!in(0, 1)) return RT_INVALID_VALUE; k->spec_walk = value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1488,6 +1528,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_GLOBAL_OCT: *value = k->global_oct; break;
         case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: *value = (int)k->pf_defer_min; break;
+        case RT_TUNE_SPEC_WALK: *value = k->spec_walk; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

@@ -101,9 +101,25 @@ struct rt_comm_s {
 
 namespace {
 
+// The communicator's transfer and unpack streams run at the device's greatest stream priority.
+// Two reasons, both read off a kernel trace of the world-1 flow (profiles/r04/dist_streams.txt):
+// * HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES 4); at normal priority these two
+//   shared the main stream's and a render stream's queue, so the next fused render sat behind the
+//   previous step's unpack, which sat behind its transfer.  High-priority streams get queues of
+//   their own.
+// * RCCL's transfer kernel needs CU slots, and a persistent render holds them all until it
+//   drains; at normal priority the next render's workgroups took the slots the draining one
+//   freed, and the transfer waited (6.4 ms for a 0.11-ms copy).  At high priority its workgroups
+//   are dispatched first.
+#ifndef RT_COMM_STREAM_PRIO
+#define RT_COMM_STREAM_PRIO 1
+#endif
 int comm_streams(rt_comm c) {
-    hipError_t e = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const int prio = RT_COMM_STREAM_PRIO ? greatest : least;
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, prio);
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipEventCreateWithFlags(&c->packed[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
@@ -270,7 +286,8 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
 }
 
 int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
-    if (!ctxs || !comms_out || n < 1) return RT_INVALID_VALUE;
+    // (check_loopback tracks the members of a call in a 64-bit mask)
+    if (!ctxs || !comms_out || n < 1 || n > 64) return RT_INVALID_VALUE;
     for (int i = 0; i < n; ++i) {
         comms_out[i] = nullptr;
         if (!ctxs[i]) return RT_INVALID_CONTEXT;
@@ -346,8 +363,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         uint8_t* out = static_cast<uint8_t*>(outs[i]->dptr);
         // the bands are final after every accumulation enqueued so far (astream, in order) and
         // after whatever the main stream has queued (per-frame launches write `out` there)
-        e = hipEventRecord(ctx->mtail, ctx->stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->astream, ctx->mtail, 0);
+        e = rti::main_tail_wait(ctx, ctx->astream);
         if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);  // slot free
         if (e == hipSuccess)
             e = copy_rects(c->plans[c->rank], out, static_cast<uint8_t*>(c->stage[s]), true, ctx->astream);
@@ -430,15 +446,22 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
         if (e != hipSuccess) return map_hip(e);
         c->sent_valid[s] = true;
         if (c->rank == root) {
+            // Gathering into the root's own output: its own bands are in place already and are
+            // not unpacked, so the unpack writes only other ranks' rows, which no later render,
+            // accumulation or pack of this context touches -- nothing on the context waits for
+            // it.  (An unpack that the next accumulation had to wait for chained that
+            // accumulation, and the render after it, to the transfer: RCCL's kernel gets CUs only
+            // as a persistent render drains, so every second render started a step late --
+            // world-1 0.90 vs 0.77 ms/frame, profiles/r04/dist_streams.txt.)  Reads of the
+            // image wait for it through the context's queue (gtail, qs()).
+            const bool into_out = !root_dst || root_dst == outs[i];
             uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
             e = hipStreamWaitEvent(c->ustream, c->sent[s], 0);
             for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-                e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
-                               false, c->ustream);
+                if (!(into_out && q == c->rank))
+                    e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
+                                   false, c->ustream);
             if (e == hipSuccess) e = hipEventRecord(c->unpacked[s], c->ustream);
-            // later accumulations on this context come after the unpack (the destination may be
-            // `out` itself: the unpack rewrites the root's own rows with the same bytes)
-            if (e == hipSuccess) e = hipStreamWaitEvent(ctx->astream, c->unpacked[s], 0);
             if (e != hipSuccess) return map_hip(e);
             c->unpacked_valid[s] = true;
         }

@@ -31,6 +31,15 @@ struct rt_context_s {
     // k's draining waves free instead of waiting for its last path
     hipStream_t rstream[RT_RAD_SETS] = {};
     hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
+    // Work may have been enqueued on the main stream since mtail was last recorded
+    // (main_tail_wait).  Streams share hardware queues (GPU_MAX_HW_QUEUES 4 < the context's and
+    // communicator's streams), so a fresh record on an idle main stream can land behind another
+    // stream's packets -- the previous step's gather transfer -- and make the next fused render
+    // wait for it.  Set by every path that enqueues there: qs() (all of them but enqueue's own
+    // launches, which set it themselves); sticky once the stream handle is exposed
+    // (rtContextGetStream), since the caller may then enqueue without telling us.
+    bool mdirty = true;
+    bool mexposed = false;
     bool apending = false;
     // host waits on the queue (rtFinish, blocking reads / writes): a per-frame launch with no wait
     // since the previous one is being queued back to back (automatic per-frame deferral)
@@ -78,7 +87,23 @@ inline hipStream_t qs(rt_context ctx) {
         (void)hipStreamWaitEvent(ctx->stream, ctx->gtail, 0);
         ctx->gpending = false;
     }
+    ctx->mdirty = true;  // the caller enqueues on it
     return ctx->stream;
+}
+
+// Make `s` wait for everything enqueued on the main stream so far.  The main stream's tail is
+// re-recorded only when something may have been enqueued there since the last record
+// (RT_MTAIL_ALWAYS: every time, the round-3 behaviour, kept for A/B builds).
+inline hipError_t main_tail_wait(rt_context ctx, hipStream_t s) {
+#ifndef RT_MTAIL_ALWAYS
+    if (ctx->mdirty || ctx->mexposed)
+#endif
+    {
+        const hipError_t e = hipEventRecord(ctx->mtail, ctx->stream);
+        if (e != hipSuccess) return e;
+        ctx->mdirty = false;
+    }
+    return hipStreamWaitEvent(s, ctx->mtail, 0);
 }
 
 // rtCommShardKernel's interleave (rt_capi.cpp): refused for a kernel with a work range

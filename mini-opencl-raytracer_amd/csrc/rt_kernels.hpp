@@ -52,6 +52,7 @@ struct KernelArgs {
     uint32_t flagTiles;
     uint32_t nFrames, radStride;
     uint32_t tileMajor;                 // fused: work items ordered (tile, frame) instead of (frame, tile)
+    uint32_t specWalk;                  // step schedule, octant walks: speculative walk (boxes nest)
     // per-frame launches (step schedule): sky-pixel shortcut key, chained launch to launch --
     // pfKeyIn = the value all-sky pixels hold if they followed the chain, pfKeyOut = this launch's
     const uint32_t* pfKeyIn;

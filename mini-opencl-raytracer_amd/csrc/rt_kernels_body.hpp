@@ -270,6 +270,23 @@ __device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelAr
     return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
 }
 
+// The same visit for the speculative walk (step_body, kSpec): `hit` and the record's two links.
+template <bool kBofs>
+__device__ __forceinline__ bool oct_probe(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                          float t, uint32_t& hn, uint32_t& mn) {
+    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+    const float4 A = sc.onodes[i], B = sc.onodes[i + (kBofs ? kOctB : a.octB)];
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    hn = __float_as_uint(B.z);
+    mn = __float_as_uint(B.w);
+    return t1 >= t0;
+}
+
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
 // early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
 // ones the reference computes where it reaches them; the rest are discarded.  A wave
@@ -657,6 +674,12 @@ __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, 
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
 constexpr uint32_t kNotWalking = 0x80000000u;  // LDS path walk word outside TRAV
+#ifndef RT_SPEC
+#define RT_SPEC 1
+#endif
+#ifndef RT_SPEC_STATS
+#define RT_SPEC_STATS 0  // diagnostic: counting builds walk speculatively too (visits = a superset)
+#endif
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -845,6 +868,22 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // at after the leaf, `leaf_i` the leaf's next triangle.
     uint32_t cur = kLdsScene ? kNotWalking : 0u;
     uint32_t leaf_i = 0u, leaf_end = 0;
+    // Speculative walk (octant walks; counting builds keep the plain walk, whose node visits are
+    // the reference's one for one).  A lane that passes a leaf does not wait there for a triangle
+    // step: the leaf's code goes to `pend` (tested by later triangle steps, one triangle each) and
+    // the walk goes on at the leaf's skip pointer with the t it has, until it passes a second leaf
+    // -- there it stops (cur = that leaf's code, >= kLeafMin; leaf_i = its node) until `pend` is
+    // done, then re-visits that node with the updated t.  So a lane in a leaf still takes node steps, and a walking
+    // lane with a pending leaf still takes triangle steps.  Same triangle tests in the same order
+    // at the same t as the reference (kernel_bvh.cl:171-219), hence the same bits: t only
+    // decreases, a box test is monotone in t and children's boxes nest in their parents'
+    // (CLBVHnode.cpp:7-159 builds them as unions), so every node the reference enters after the
+    // pending leaf the walk enters too, every leaf it skipped on the way fails for the reference
+    // as well, and the stop node is re-tested at the reference's t before its triangles.  Extra
+    // work: node visits the reference would have skipped (rt_capi.cpp checks the nesting on the
+    // host and walks plainly when a tree breaks it).
+    constexpr bool kSpec = RT_SPEC && kLdsScene && (!kStats || RT_SPEC_STATS);
+    uint32_t pend = 0u;  // (kSpec) pending leaf code count << 24 | first while >= kLeafMin
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
@@ -1153,7 +1192,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         // bodies for a mix of lanes.
         for (;;) {
             uint32_t n_trav, n_leaf;
-            if (kLdsScene) {
+            if (kSpec && a.specWalk) {
+                // walk at END with no leaf pending: the reference's traversal is over
+                if (cur == a.nNodes && pend < kLeafMin) {
+                    state = kShade;
+                    cur = kNotWalking;
+                }
+                n_trav = popc_ballot(cur < a.nNodes);  // (END lanes only wait for their triangles)
+                n_leaf = popc_ballot(pend >= kLeafMin);
+            } else if (kLdsScene) {
                 // a walk parked on the END sentinel has finished the reference's traversal
                 // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
                 if (cur == a.nNodes) {
@@ -1184,7 +1231,37 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
             constexpr int kNodeBurst = kGlobalOct ? RT_ONODE_BURST : kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
             constexpr int kTriBurst = kGlobalOct ? RT_OTRI_BURST : kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
-            if (!leaf_step) {
+            if (kSpec && a.specWalk && !leaf_step) {
+                // (t does not change during node steps: quieted once, not at every visit's min)
+                const float tq = __builtin_canonicalizef(h.t);
+#pragma unroll
+                for (int rep = 0; rep < kNodeBurst; ++rep) {
+                    if (cur < kLeafMin) {  // walking (END: the sentinel, always missed)
+                        if (kStats && cur != a.nNodes) ++st.visits;
+                        uint32_t hn, mn;
+                        const bool hit = oct_probe<kBofs>(sc, a, cur, ray, tq, hn, mn);
+                        // a passed leaf with none pending becomes the pending one (walk on at its
+                        // skip pointer); a second one stops the walk: cur = its code, leaf_i = it
+                        const bool take = hit && hn >= kLeafMin && pend < kLeafMin;
+                        leaf_i = cur;
+                        pend = take ? hn : pend;
+                        cur = hit && !take ? hn : mn;
+                    }
+                }
+            } else if (kSpec && a.specWalk) {
+#pragma unroll
+                for (int rep = 0; rep < kTriBurst; ++rep) {
+                    if (pend >= kLeafMin) {
+                        if (kStats) ++st.tests;
+                        const uint32_t idx = pend & 0x00ffffffu;
+                        ray_triangle<M, false>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
+                        pend += 1u - kLeafMin;
+                        // leaf done and the walk stopped at a second one: re-visit that node at
+                        // the new t
+                        if (pend < kLeafMin && cur >= kLeafMin) cur = leaf_i;
+                    }
+                }
+            } else if (!leaf_step) {
 #pragma unroll
                 for (int rep = 0; rep < kNodeBurst; ++rep) {
                     if (kLdsScene) {

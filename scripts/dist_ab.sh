@@ -1,0 +1,35 @@
+#!/bin/bash
+# The bench's N > 1 flow at world size 1 (RCCL communicator, pack / self-send / unpack every step,
+# pipelined with the next step) against the same bench without the gather, for the main build and
+# every library variant (lib/variants/librt_hip_*.so), REPS interleaved rounds; then one
+# rocprofv3 kernel + memory-copy trace of the flow per build (scripts/stream_timeline.py reads it).
+# usage: scripts/dist_ab.sh [REPS] [bench args...]
+set -u
+OUT=gpurun_out/dist_ab
+mkdir -p $OUT
+export TMPDIR=/tmp
+reps=${1:-2}; shift || true
+V=mini-opencl-raytracer_amd/lib/variants
+libs="main $(ls $V 2>/dev/null | sed -n 's/^librt_hip_\(.*\)\.so$/\1/p')"
+run() {  # run <name> <args...>
+  local name=$1; shift
+  timeout -k 10 120 python bench.py --no-cpu-baseline --no-drop-in --steps 20 --warmup 2 "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "FAILED $name"; tail -5 $OUT/$name.err; exit 1; }
+  python3 -c "
+import json
+d = json.loads([l for l in open('$OUT/$name.json') if l.startswith('{')][-1])
+print('$name', d['ms_per_frame'], d['roofline'].get('launch_ms'), d.get('check_gather', ''))" | tee -a $OUT/summary.txt
+}
+for rep in $(seq $reps); do
+  for l in $libs; do
+    if [ $l = main ]; then unset RT_HIP_LIB; else export RT_HIP_LIB=$V/librt_hip_$l.so; fi
+    run ${l}_nodist_$rep "$@"
+    run ${l}_dist_$rep --force-dist --check-gather "$@"
+  done
+done
+for l in $libs; do
+  if [ $l = main ]; then unset RT_HIP_LIB; else export RT_HIP_LIB=$V/librt_hip_$l.so; fi
+  timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_$l -o run -- \
+    python bench.py --no-cpu-baseline --no-drop-in --steps 5 --warmup 1 --force-dist "$@" > $OUT/trace_$l.log 2>&1 || { echo "trace $l failed"; tail -5 $OUT/trace_$l.log; exit 1; }
+  python3 scripts/stream_timeline.py $OUT/trace_$l --last 60 > $OUT/timeline_$l.txt 2>&1
+  tail -3 $OUT/timeline_$l.txt
+done

@@ -52,8 +52,9 @@ def test_device_bvh_structure(max_prims, method):
 def test_device_bvh_single_leaf(n, method):
     tris, mats = _file_order_cornell()
     sc = S.build_bvh_device(tris[:n], mats, 4, method=method)
-    if n == 1 or method == "lbvh":  # (PLOC keeps a small set split where the SAH prefers it, as
-        assert sc.nodes.shape[0] == 1 and sc.nodes[0]["nPrimitives"] == n  # the reference's build does)
+    # n <= max_prims: one leaf, for both builders (PLOC collapses every subtree of <= max_prims
+    # triangles; only an RT_PLOC_SAH_LEAVES build, off by default, lets the SAH keep it split)
+    assert sc.nodes.shape[0] == 1 and sc.nodes[0]["nPrimitives"] == n
     assert sc.nodes["nPrimitives"].sum() == n
     _check_bvh(sc)
 
