@@ -18,6 +18,9 @@ LIB = os.path.join(REF_DIR, "libclref.so")
 VARIANTS = {
     "strict": os.path.join(REF_DIR, "kernel_bvh_strict.co"),
     "shipped": os.path.join(REF_DIR, "kernel_bvh_shipped.co"),
+    # built by the OpenCL runtime itself from source, as the reference host does
+    # (oracle/offline_build.c: clBuildProgram(" -I . ") for an offline gfx950 device)
+    "runtime": os.path.join(REF_DIR, "kernel_bvh_runtime.co"),
 }
 
 
