@@ -607,8 +607,16 @@ int rtCreateContext(int device_index, rt_context* out) {
         return RT_INVALID_COMMAND_QUEUE;
     }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device_index) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (hipGetDeviceProperties(&prop, device_index) == hipSuccess) {
+        c->num_cus = prop.multiProcessorCount;
+        // MI300-class parts: 8 XCDs, CU-mask bits interleaved across them
+        // (scripts/probes/cu_mask_probe.hip, profiles/r04/cu_mask_probe.txt)
+        if ((std::strncmp(prop.gcnArchName, "gfx94", 5) == 0 || std::strncmp(prop.gcnArchName, "gfx95", 5) == 0) &&
+            c->num_cus % 8 == 0)
+            c->n_xcd = 8;
+    }
     if (c->num_cus <= 0) c->num_cus = 256;
+    c->render_cus = c->num_cus;
     *out = c;
     return RT_SUCCESS;
 }
@@ -1006,7 +1014,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct);
         k->occ_smem[si][mi][lds][k->stats][var] = smem;
     }
-    uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) * (uint64_t)ctx->num_cus;
+    // (a render stream may exclude CUs an RCCL communicator reserved: rti::reserve_cus)
+    const bool on_rstream = rstr != ctx->stream;
+    uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) *
+                    (uint64_t)(on_rstream ? ctx->render_cus : ctx->num_cus);
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
     // (wavefront extend: 8 waves per workgroup)
     grid = std::min<uint64_t>(grid, si == RT_SCHED_TILES ? n_tiles
@@ -1454,6 +1465,47 @@ int rtContextGetStream(rt_context ctx, void** s) {
     *s = qs(ctx);
     return RT_SUCCESS;
 }
+
+}  // extern "C"
+
+namespace rti {
+
+int reserve_cus(rt_context ctx, int per_xcd, std::vector<uint32_t>* comm_mask) {
+    const int per = ctx->num_cus / ctx->n_xcd;
+    if (per_xcd < 0 || per_xcd >= per) return RT_INVALID_VALUE;
+    const size_t words = (size_t)(ctx->num_cus + 31) / 32;
+    std::vector<uint32_t> all(words, 0u), res(words, 0u);
+    for (int b = 0; b < ctx->num_cus; ++b) {
+        all[b / 32] |= 1u << (b % 32);
+        // the last per_xcd CUs of each XCD: bit = cu * n_xcd + xcd
+        if (b / ctx->n_xcd >= per - per_xcd) res[b / 32] |= 1u << (b % 32);
+    }
+    if (comm_mask) *comm_mask = res;
+    if (per_xcd == ctx->reserved_per_xcd) return RT_SUCCESS;
+    // re-create the render streams on the remaining CUs, once their work is done
+    hipError_t e = hipSuccess;
+    for (hipStream_t& r : ctx->rstream) {
+        if (e == hipSuccess) e = hipStreamSynchronize(r);
+        if (e != hipSuccess) break;
+        (void)hipStreamDestroy(r);
+        r = nullptr;
+        if (per_xcd == 0) {
+            e = hipStreamCreateWithFlags(&r, hipStreamNonBlocking);
+        } else {
+            std::vector<uint32_t> m(words);
+            for (size_t w = 0; w < words; ++w) m[w] = all[w] & ~res[w];
+            e = hipExtStreamCreateWithCUMask(&r, (uint32_t)words, m.data());
+        }
+    }
+    if (e != hipSuccess) return map_hip(e);
+    ctx->reserved_per_xcd = per_xcd;
+    ctx->render_cus = ctx->num_cus - per_xcd * ctx->n_xcd;
+    return RT_SUCCESS;
+}
+
+}  // namespace rti
+
+extern "C" {
 
 int rtContextGetDevice(rt_context ctx, int* d) {
     if (!ctx || !d) return RT_INVALID_VALUE;

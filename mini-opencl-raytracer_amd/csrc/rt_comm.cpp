@@ -83,6 +83,7 @@ struct rt_comm_s {
     // members) and the transfer is a device copy on the root's communicator stream
     const void* group = nullptr;
     hipEvent_t xfer = nullptr;  // root: the copies of one gather done
+    bool reserved = false;      // holds a CU reservation on ctx (rti::reserve_cus)
     int rank = 0, nranks = 1;
     hipStream_t cstream = nullptr;  // RCCL
     hipStream_t ustream = nullptr;  // root: unpack
@@ -114,12 +115,36 @@ namespace {
 #ifndef RT_COMM_STREAM_PRIO
 #define RT_COMM_STREAM_PRIO 1
 #endif
-int comm_streams(rt_comm c) {
+// RCCL communicators: CUs of every XCD kept for the communicator's streams (rti::reserve_cus).
+// RCCL's transfer kernel (64 workgroups of 256 threads, 37 KB of LDS and 248 VGPRs each on
+// gfx950) does not fit beside a persistent render on any CU, so without a reservation it runs
+// only where renders drain (profiles/r04/dist_streams.txt); with one it runs at once on its own
+// CUs, and the renders lose those CUs' share (1 per XCD = 8 of 256 = 3 %).  0 = none.
+int comm_events(rt_comm c, hipError_t e);
+#ifndef RT_COMM_RESERVE_PER_XCD
+#define RT_COMM_RESERVE_PER_XCD 1
+#endif
+int comm_streams(rt_comm c, bool rccl) {
+    hipError_t e = hipSuccess;
+    if (rccl && RT_COMM_RESERVE_PER_XCD > 0) {
+        std::vector<uint32_t> mask;
+        int rc = rti::reserve_cus(c->ctx, RT_COMM_RESERVE_PER_XCD, &mask);
+        if (rc) return rc;
+        c->reserved = true;
+        ++c->ctx->reserve_refs;
+        e = hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)mask.size(), mask.data());
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->ustream, (uint32_t)mask.size(), mask.data());
+        return comm_events(c, e);
+    }
     int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     const int prio = RT_COMM_STREAM_PRIO ? greatest : least;
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, prio);
+    return comm_events(c, e);
+}
+
+int comm_events(rt_comm c, hipError_t e) {
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipEventCreateWithFlags(&c->packed[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
@@ -154,6 +179,8 @@ void release(rt_comm c) {
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
+    // the last communicator of the context gives its CUs back to the renders
+    if (c->reserved && --c->ctx->reserve_refs == 0) (void)rti::reserve_cus(c->ctx, 0, nullptr);
     delete c;
 }
 
@@ -235,7 +262,7 @@ int rtCommInitRank(rt_context ctx, int nranks, const void* id, int rank, rt_comm
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     int rc = map_nccl(ncclCommInitRank(&c->nc, nranks, u, rank));
-    if (!rc) rc = comm_streams(c);
+    if (!rc) rc = comm_streams(c, true);
     if (rc) {
         release(c);
         return rc;
@@ -264,7 +291,7 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
             c->rank = i;
             c->nranks = n;
             (void)hipSetDevice(ctxs[i]->device);
-            rc = comm_streams(c);
+            rc = comm_streams(c, true);
         } else {
             (void)ncclCommDestroy(nc[i]);
             nc[i] = nullptr;
@@ -303,7 +330,7 @@ int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
             c->rank = i;
             c->nranks = n;
             hipError_t e = hipSetDevice(ctxs[i]->device);
-            rc = e == hipSuccess ? comm_streams(c) : map_hip(e);
+            rc = e == hipSuccess ? comm_streams(c, false) : map_hip(e);
         }
         if (rc) {
             if (c) release(c);

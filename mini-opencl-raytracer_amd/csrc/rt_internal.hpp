@@ -20,6 +20,12 @@ struct rt_context_s {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 0;
+    // CUs the render streams (rstream) may use: num_cus, unless an RCCL communicator reserved some
+    // for its transfer kernels (rti::reserve_cus); fused renders size their persistent grid by it
+    int render_cus = 0;
+    int reserved_per_xcd = 0;
+    int reserve_refs = 0;  // communicators holding the reservation
+    int n_xcd = 1;  // XCDs (CU-mask bit b selects CU b / n_xcd of XCD b % n_xcd)
     // Fused frames: the accumulation launch runs on its own stream, so it overlaps the next
     // render (its waves fit beside the render grid: RT_ACCUM_VGPRS).  Every other operation
     // goes through qs(), which first makes the context's in-order stream wait for the
@@ -108,5 +114,11 @@ inline hipError_t main_tail_wait(rt_context ctx, hipStream_t s) {
 
 // rtCommShardKernel's interleave (rt_capi.cpp): refused for a kernel with a work range
 int shard_kernel(rt_kernel k, unsigned period, unsigned phase);
+
+// Reserve `per_xcd` CUs of every XCD for a communicator (rt_capi.cpp): the context's render
+// streams are re-created without them (after draining), fused renders size their grid to the
+// rest, and `comm_mask` receives the reserved CUs' mask for the communicator's streams
+// (hipExtStreamCreateWithCUMask words).  per_xcd 0 releases the reservation.
+int reserve_cus(rt_context ctx, int per_xcd, std::vector<uint32_t>* comm_mask);
 
 }  // namespace rti

@@ -882,7 +882,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // as well, and the stop node is re-tested at the reference's t before its triangles.  Extra
     // work: node visits the reference would have skipped (rt_capi.cpp checks the nesting on the
     // host and walks plainly when a tree breaks it).
-    constexpr bool kSpec = RT_SPEC && kLdsScene && (!kStats || RT_SPEC_STATS);
+    // (LDS scenes only: on the octant walk over HBM/L2 the extra visits cost address-unit load
+    // instructions, that walk's binding resource -- bunny proxy +12 %, profiles/r04/spec_walk.txt)
+    constexpr bool kSpec = RT_SPEC && kLdsScene && !kGlobalOct && (!kStats || RT_SPEC_STATS);
     uint32_t pend = 0u;  // (kSpec) pending leaf code count << 24 | first while >= kLeafMin
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
@@ -1241,11 +1243,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         uint32_t hn, mn;
                         const bool hit = oct_probe<kBofs>(sc, a, cur, ray, tq, hn, mn);
                         // a passed leaf with none pending becomes the pending one (walk on at its
-                        // skip pointer); a second one stops the walk: cur = its code, leaf_i = it
-                        const bool take = hit && hn >= kLeafMin && pend < kLeafMin;
+                        // skip pointer); a second one stops the walk: cur = its code, leaf_i = it.
+                        // The successor on a hit is chosen from the record and `pend` alone, so
+                        // the box test's result feeds one select, as in the plain walk (the walk
+                        // is a dependent chain: latency, not issue, is its cost)
+                        const bool leaf_free = hn >= kLeafMin && pend < kLeafMin;
+                        const uint32_t on_hit = leaf_free ? mn : hn;
                         leaf_i = cur;
-                        pend = take ? hn : pend;
-                        cur = hit && !take ? hn : mn;
+                        pend = hit && leaf_free ? hn : pend;
+                        cur = hit ? on_hit : mn;
                     }
                 }
             } else if (kSpec && a.specWalk) {

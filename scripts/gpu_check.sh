@@ -37,6 +37,29 @@ for step in "$@"; do
     phase) run phase 300 python scripts/phase_profile.py ;;
     phasebunny) RT_PHASE_SCENE=bunny run phase_bunny 300 python scripts/phase_profile.py ;;
     refgold) run refgold 900 python scripts/make_ref_goldens.py gpurun_out/golden ;;
+    # the round's final record (what the round-3 final_r03_{a,b,c,d}.sh did, by step):
+    #   final_suite: GPU suite (long per-test limit) + smoke on the final build
+    final_suite) run pytest_gpu 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread && \
+                 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    #   final_bench: PMC records (headline + bunny -> profiles/pmc.json), the default bench with its CPU
+    #   baseline and drop-in figures, and a kernel trace of the timed loop
+    final_bench) run pmc_default 900 bash scripts/profile.sh default && \
+                 run pmc_bunny 900 bash scripts/profile.sh bunny --scene bunny && \
+                 cp gpurun_out/pmc_bunny/pmc.json profiles/pmc.json && \
+                 run bench_default 600 python bench.py && \
+                 run bench_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/final_trace -o run -- python bench.py --steps 20 --warmup 1 --no-cpu-baseline --no-drop-in ;;
+    #   final_configs: the other configs (no CPU baseline / drop-in) and the emulated ranks
+    final_configs) for c in "bunny --scene bunny" "perframe --launch per-frame --steps 5" "pinned --math pinned --steps 5" \
+                             "1080p --width 1920 --height 1080 --bounces 2 --frames 1 --steps 20" \
+                             "512 --width 512 --height 512 --bounces 1 --frames 1 --steps 50" \
+                             "bunny_perframe --scene bunny --launch per-frame --steps 3"; do
+                     set -- $c; n=$1; shift
+                     run bench_$n 300 python bench.py --no-cpu-baseline --no-drop-in "$@"
+                   done
+                   for sc in cornell bunny; do
+                     RT_EMU_SCENE=$sc run rank_emulation_$sc 600 python scripts/rank_emulation.py
+                     RT_EMU_SCENE=$sc RT_EMU_GATHER=1 run rank_emulation_gather_$sc 900 python scripts/rank_emulation.py 1 8
+                   done ;;
     configs) run cfg3_default 600 python bench.py && \
              run cfg3_pinned 300 python bench.py --math pinned --no-cpu-baseline && \
              run cfg2_1080p 300 python bench.py --width 1920 --height 1080 --bounces 2 --frames 1 --steps 20 --no-cpu-baseline && \
