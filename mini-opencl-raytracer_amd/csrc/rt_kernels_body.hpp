@@ -721,6 +721,13 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
 #endif
+// shade early when at most RT_TRAV_LOW lanes are still walking and at least RT_SHADE_LOW wait
+#ifndef RT_TRAV_LOW
+#define RT_TRAV_LOW 0
+#endif
+#ifndef RT_SHADE_LOW
+#define RT_SHADE_LOW 24
+#endif
 
 
 // the same for scenes read from HBM/L2 (global path)
@@ -1216,7 +1223,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 n_leaf = popc_ballot(state == kLeaf);
             }
             if (n_trav + n_leaf == 0u) break;
-            if (popc_ballot(state == kShade) >= kShadeMin) break;
+            {
+                const uint32_t n_shade = popc_ballot(state == kShade);
+                if (n_shade >= kShadeMin) break;
+                // few lanes left walking while many wait to shade: their traversal steps would
+                // run nearly empty, so shade the waiting batch now (RT_TRAV_LOW 0: off)
+                if (RT_TRAV_LOW > 0 && n_trav + n_leaf <= RT_TRAV_LOW && n_shade >= RT_SHADE_LOW) break;
+            }
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
             if (kStats) {

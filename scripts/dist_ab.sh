@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 reps=${1:-2}; shift || true
 V=mini-opencl-raytracer_amd/lib/variants
-libs="main $(ls $V 2>/dev/null | sed -n 's/^librt_hip_\(.*\)\.so$/\1/p')"
+libs=${DIST_LIBS:-"main $(ls $V 2>/dev/null | sed -n 's/^librt_hip_\(.*\)\.so$/\1/p')"}  # DIST_LIBS: a subset
 run() {  # run <name> <args...>
   local name=$1; shift
   timeout -k 10 120 python bench.py --no-cpu-baseline --no-drop-in --steps 20 --warmup 2 "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "FAILED $name"; tail -5 $OUT/$name.err; exit 1; }
