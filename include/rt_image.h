@@ -26,6 +26,16 @@ int rtiWritePPM(const char* path, const float* px, unsigned W, unsigned H);
 /* PNG, 8-bit RGB, zlib stream of stored (uncompressed) deflate blocks: no external library. */
 int rtiWritePNG(const char* path, const float* px, unsigned W, unsigned H);
 
+/* Checkpoint / resume of a progressive render: the reference's whole render state is
+ * its accumulation buffer plus m_FrameCount (CLRaytracer.h:30-37; KernelEntry accumulates in place,
+ * kernel_bvh.cl:449-455), so a run of N spp can stop after frame f and go on later from the same
+ * bits.  Format: "RTACCUM1", u32 W, u32 H, u32 next frame count, the W*H float4 pixels as stored
+ * (16-byte stride, 4th lane included), u64 FNV-1a of everything before it.
+ * rtiLoadAccum with px == NULL only reads the header (W, H, next frame); a bad magic, size or
+ * checksum is RT_PARSE_ERROR, a W x H that differs from the caller's (px != NULL) RT_INVALID_VALUE. */
+int rtiSaveAccum(const char* path, const float* px, unsigned W, unsigned H, unsigned next_frame);
+int rtiLoadAccum(const char* path, float* px, unsigned* W, unsigned* H, unsigned* next_frame);
+
 #ifdef __cplusplus
 }
 #endif

@@ -106,6 +106,25 @@ class Raytracer:
         w = image.write_png if path.lower().endswith(".png") else image.write_ppm
         w(path, self.pixels, self.width, self.height)
 
+    def checkpoint(self, path: str) -> None:
+        """Save the render state -- the accumulation buffer and m_FrameCount (include/rt_image.h
+        rtiSaveAccum) -- so a progressive render can resume later from the same bits."""
+        from . import image
+        px = np.empty((self.height * self.width, 4), np.float32)
+        self.ctx.ReadBuffer(self.output, px, blocking=True)
+        image.save_accum(path, px, self.width, self.height, self.frame_count)
+
+    def resume(self, path: str) -> None:
+        """Restore a checkpoint into this (initialised) raytracer: the next RenderFrame continues
+        the accumulation exactly where the saved run stopped."""
+        from . import image
+        px, nf = image.load_accum(path)
+        if px.shape[0] != self.width * self.height:
+            raise ValueError("checkpoint size differs from this raytracer's")
+        self.ctx.WriteBuffer(self.output, px)
+        self.pixels[:] = px
+        self.frame_count = nf
+
     def release(self) -> None:
         for b in self._scene_bufs:
             b.release()

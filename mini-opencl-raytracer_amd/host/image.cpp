@@ -124,3 +124,76 @@ extern "C" int rtiWritePNG(const char* path, const float* px, unsigned W, unsign
     chunk(f, "IEND", {});
     return std::fclose(f) == 0 ? RT_SUCCESS : RT_OUT_OF_RESOURCES;
 }
+
+// ---- accumulation checkpoint (rtiSaveAccum / rtiLoadAccum) ----------------------------------
+namespace {
+
+constexpr char kAccumMagic[8] = {'R', 'T', 'A', 'C', 'C', 'U', 'M', '1'};
+
+uint64_t fnv1a64(const void* p, size_t n, uint64_t h) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+}  // namespace
+
+extern "C" int rtiSaveAccum(const char* path, const float* px, unsigned W, unsigned H, unsigned next_frame) {
+    if (!path || !px || W == 0 || H == 0) return RT_INVALID_VALUE;
+    const uint32_t hdr[3] = {W, H, next_frame};
+    const size_t bytes = (size_t)W * H * 16;
+    uint64_t h = 14695981039346656037ull;
+    h = fnv1a64(kAccumMagic, 8, h);
+    h = fnv1a64(hdr, sizeof(hdr), h);
+    h = fnv1a64(px, bytes, h);
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return RT_INVALID_VALUE;
+    bool ok = std::fwrite(kAccumMagic, 1, 8, f) == 8 && std::fwrite(hdr, sizeof(hdr), 1, f) == 1 &&
+              std::fwrite(px, 1, bytes, f) == bytes && std::fwrite(&h, sizeof(h), 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_SUCCESS : RT_OUT_OF_RESOURCES;
+}
+
+extern "C" int rtiLoadAccum(const char* path, float* px, unsigned* W, unsigned* H, unsigned* next_frame) {
+    if (!path || !W || !H || !next_frame) return RT_INVALID_VALUE;
+    std::FILE* f = std::fopen(path, "rb");
+    if (!f) return RT_FILE_NOT_FOUND;
+    char magic[8];
+    uint32_t hdr[3];
+    int rc = RT_SUCCESS;
+    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kAccumMagic, 8) != 0 ||
+        std::fread(hdr, sizeof(hdr), 1, f) != 1 || hdr[0] == 0 || hdr[1] == 0)
+        rc = RT_PARSE_ERROR;
+    const size_t bytes = rc ? 0 : (size_t)hdr[0] * hdr[1] * 16;
+    if (!rc) {
+        // the file holds exactly header + pixels + checksum
+        if (std::fseek(f, 0, SEEK_END) != 0 || std::ftell(f) != (long)(8 + sizeof(hdr) + bytes + 8) ||
+            std::fseek(f, 8 + sizeof(hdr), SEEK_SET) != 0)
+            rc = RT_PARSE_ERROR;
+    }
+    if (!rc && px) {
+        if (hdr[0] != *W || hdr[1] != *H) {
+            rc = RT_INVALID_VALUE;
+        } else {
+            uint64_t stored = 0, h = 14695981039346656037ull;
+            if (std::fread(px, 1, bytes, f) != bytes || std::fread(&stored, sizeof(stored), 1, f) != 1) {
+                rc = RT_PARSE_ERROR;
+            } else {
+                h = fnv1a64(kAccumMagic, 8, h);
+                h = fnv1a64(hdr, sizeof(hdr), h);
+                h = fnv1a64(px, bytes, h);
+                if (h != stored) rc = RT_PARSE_ERROR;
+            }
+        }
+    }
+    std::fclose(f);
+    if (rc) return rc;
+    *W = hdr[0];
+    *H = hdr[1];
+    *next_frame = hdr[2];
+    return RT_SUCCESS;
+}
+

@@ -79,3 +79,33 @@ def test_errors(tmp_path):
         image.write_png(str(tmp_path / "x.png"), np.zeros(5, np.float32), 2, 2)
     with pytest.raises(RTError):
         image.write_png(str(tmp_path / "no" / "dir.png"), np.zeros((4, 4), np.float32), 2, 2)
+
+
+# ---- checkpoint / resume of the accumulation buffer (rtiSaveAccum / rtiLoadAccum) ----------------
+def test_accum_checkpoint_round_trip(tmp_path):
+    W, H = 13, 9
+    px = _buf(W, H, seed=5)
+    px[:, 3] = np.arange(W * H, dtype=np.float32)  # the 4th lane travels too (16-byte stride)
+    p = str(tmp_path / "a.rtaccum")
+    image.save_accum(p, px, W, H, 5)
+    got, nf = image.load_accum(p)
+    assert nf == 5
+    assert got.tobytes() == px.tobytes()  # NaN / inf bits included
+
+
+def test_accum_checkpoint_rejects_damage(tmp_path):
+    W, H = 4, 3
+    p = tmp_path / "a.rtaccum"
+    image.save_accum(str(p), _buf(W, H), W, H, 2)
+    raw = bytearray(p.read_bytes())
+    raw[40] ^= 1  # a pixel bit
+    bad = tmp_path / "bad.rtaccum"
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(RTError):
+        image.load_accum(str(bad))
+    short = tmp_path / "short.rtaccum"
+    short.write_bytes(p.read_bytes()[:-9])
+    with pytest.raises(RTError):
+        image.load_accum(str(short))
+    with pytest.raises(RTError):
+        image.load_accum(str(tmp_path / "missing.rtaccum"))
