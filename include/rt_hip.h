@@ -293,10 +293,12 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   PERFRAME_DEFER_MIN                work items from which PERFRAME_DEFER 2 defers (default 4 Mi)
  *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
  *                                     as many as fit, default; fewer = fewer waves per SIMD)
- *   SPEC_WALK                         step schedule, octant walks: 1 (default) = speculative walk
- *                                     (a lane walks on past a passed leaf while its triangles are
- *                                     pending; same bits), 0 = the plain walk.  Trees whose child
- *                                     boxes do not nest in their parents' always walk plainly. */
+ *   SPEC_WALK                         step schedule, LDS octant walk, builds with the speculative
+ *                                     walk compiled in (RT_SPEC=1; the shipped build has it out,
+ *                                     measured slower): 1 (default) = speculative walk (a lane
+ *                                     walks on past a passed leaf while its triangles are pending;
+ *                                     same bits), 0 = the plain walk.  Trees whose child boxes do
+ *                                     not nest in their parents' always walk plainly. */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,

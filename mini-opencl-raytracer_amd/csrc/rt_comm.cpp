@@ -122,7 +122,7 @@ namespace {
 // CUs, and the renders lose those CUs' share (1 per XCD = 8 of 256 = 3 %).  0 = none.
 int comm_events(rt_comm c, hipError_t e);
 #ifndef RT_COMM_RESERVE_PER_XCD
-#define RT_COMM_RESERVE_PER_XCD 1
+#define RT_COMM_RESERVE_PER_XCD 0
 #endif
 int comm_streams(rt_comm c, bool rccl) {
     hipError_t e = hipSuccess;
@@ -216,13 +216,18 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root) {
     return RT_SUCCESS;
 }
 
+// pack / unpack copies on the copy engines (hipMemcpyDeviceToDeviceNoCU) instead of blit kernels
+#ifndef RT_COMM_NOCU
+#define RT_COMM_NOCU 0
+#endif
 hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* stage, bool to_stage, hipStream_t s) {
+    const hipMemcpyKind kind = RT_COMM_NOCU ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
     for (const rt_rect& r : plan) {
         hipError_t e = to_stage
             ? hipMemcpy2DAsync(stage + r.stage_offset, r.width, img + r.img_offset, r.img_pitch, r.width, r.rows,
-                               hipMemcpyDeviceToDevice, s)
+                               kind, s)
             : hipMemcpy2DAsync(img + r.img_offset, r.img_pitch, stage + r.stage_offset, r.width, r.width, r.rows,
-                               hipMemcpyDeviceToDevice, s);
+                               kind, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -674,8 +674,11 @@ __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, 
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
 constexpr uint32_t kNotWalking = 0x80000000u;  // LDS path walk word outside TRAV
+// speculative walk compiled in (RT_TUNE_SPEC_WALK then picks it per kernel).  Off: on the 4K
+// Cornell headline the build with it ran 0.824 ms/frame speculating and 0.841 with the knob at 0,
+// against 0.767 without the code (profiles/r04/spec_walk_ab.txt)
 #ifndef RT_SPEC
-#define RT_SPEC 1
+#define RT_SPEC 0
 #endif
 #ifndef RT_SPEC_STATS
 #define RT_SPEC_STATS 0  // diagnostic: counting builds walk speculatively too (visits = a superset)
