@@ -96,6 +96,9 @@ def parse():
                    help="N>1: wait for each step's gather before queueing the next step (no pipelining)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 flow (RCCL communicator + gather) even at WORLD_SIZE 1")
+    p.add_argument("--transport", choices=["copy", "rccl"], default="copy",
+                   help="N>1: how the gather moves the bands (rtCommSetTransport): copy engines over xGMI "
+                        "(default) or RCCL send/recv kernels")
     p.add_argument("--check-gather", action="store_true",
                    help="after timing, rank 0 renders the whole frame unsharded and checks the gathered "
                         "image against it byte for byte")
@@ -334,6 +337,14 @@ def main():
         if rank == 0:
             mg.rendezvous_cleanup()
     r = Rank(scene, args, local, comm)
+    # the root assembles the image in a buffer of its own (an application's display image): the
+    # gather then moves every rank's bands, the root's own included, so a world of one runs the
+    # whole data path (pack, transfer, unpack)
+    img = None
+    if comm is not None:
+        comm.set_transport(N.COMM_TRANSPORT_RCCL if args.transport == "rccl" else N.COMM_TRANSPORT_COPY_ENGINES)
+        if rank == 0:
+            img = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16)
 
     # instrumented pass: ray / node / triangle / hit counts of one step on this rank
     st = count_pass(r)
@@ -345,7 +356,7 @@ def main():
     def step():
         r.render()  # steps are queued back to back (sync only around the timed region)
         if comm is not None:
-            mg.Comm.gather_bands([comm], [r.out], r.W, r.H, root=0)
+            mg.Comm.gather_bands([comm], [r.out], r.W, r.H, root=0, dst=img)
             if args.gather_sync:
                 r.finish()
 
@@ -373,7 +384,7 @@ def main():
     if args.check_gather and comm is not None and rank == 0:
         # the gathered image (every rank's bands, through RCCL) against an unsharded render
         a = np.empty((r.H * r.W, 4), np.float32)
-        r.ctx.ReadBuffer(r.out, a, blocking=True)
+        r.ctx.ReadBuffer(img, a, blocking=True)
         ref_out = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16)
         kf = make_kernel(r.ctx, r.bufs, ref_out, args)
         r.render(kf)
@@ -423,7 +434,8 @@ def main():
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
                    "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh,
                    "parallelism": f"interleaved 8-row bands x{world}" + (
-                       " + RCCL gather to rank 0 (librt_hip rtCommEnqueueGatherBands"
+                       f" + gather to rank 0 over {'RCCL' if args.transport == 'rccl' else 'copy engines'}"
+                       " (librt_hip rtCommEnqueueGatherBands"
                        + (", host-synchronised)" if args.gather_sync else ", pipelined with the next step)")
                        if comm is not None else ""),
                    "rays_per_step": int(rays_per_step), "samples_per_step": args.width * args.height * args.frames,

@@ -334,8 +334,8 @@ int rtContextSetAccumOverlap(rt_context ctx, int enable);
  * are independent -- the seed depends only on the global work-item id and frameCount
  * (kernel_bvh.cl:445) and the accumulation is per pixel (:449-455) -- so a frame shards by
  * interleaved 8-row bands (band b -> rank b % nranks; rtCommShardKernel) rendered at their
- * global positions, with one exchange at the end: the bands are gathered to a root rank over
- * RCCL (xGMI), byte-identical to a one-GPU render.
+ * global positions, with one exchange at the end: the bands are gathered to a root rank (copy
+ * engines over xGMI, or RCCL; rtCommSetTransport), byte-identical to a one-GPU render.
  *
  * Communicators: one rank per GPU, either one process per GPU (rtCommGetUniqueId on one rank,
  * the 128-byte id passed to the others by any host means, rtCommInitRank everywhere) or one
@@ -362,16 +362,31 @@ int rtCommShardKernel(rt_comm comm, rt_kernel k);
  * the root's own `out`).  `comms`/`outs`: the n_local communicators this host thread drives
  * (1 per process in the one-process-per-GPU setup) and their output buffers.  Asynchronous and
  * pipelined: each rank packs its bands after the fused-frame accumulations enqueued so far (on
- * the context's accumulation stream), RCCL moves them (grouped send/recv: the root receives on
- * all links at once; its own bands go through RCCL too, a device-local send to itself, so a
- * world of one runs the same flow) on the communicator's stream and the root unpacks them on a
- * third stream (gathering into its own `out`, the root's own bands are in place and not
- * unpacked), so neither the next fused render nor the next accumulation is held up by the
- * transfer; two staging slots, so step k's gather overlaps step k+1's render.  The
- * communicator's streams run at the device's greatest stream priority.  Every later call on a context that reads or writes memory (rtFinish,
- * rtEnqueueReadBuffer, per-frame launches, ...) is ordered after the gather. */
+ * the context's accumulation stream), the transport (rtCommSetTransport) moves them to the root
+ * on the communicator's stream, and the root unpacks them on a third stream (gathering into its
+ * own `out`, the root's own bands are in place: it neither sends nor unpacks them), so neither
+ * the next fused render nor the next accumulation is held up by the transfer; two staging
+ * slots, so step k's gather overlaps step k+1's render.  The communicator's streams run at the
+ * device's greatest stream priority.  Every later call on a context that reads or writes memory
+ * (rtFinish, rtEnqueueReadBuffer, per-frame launches, ...) is ordered after the gather. */
 int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_local, unsigned width,
                              unsigned height, int root, rt_mem root_dst);
+/* How the gather moves the packed bands (set alike on every rank, before a gather; a change
+ * takes effect at the next gather, which rebuilds the plan -- a collective step):
+ *   RT_COMM_TRANSPORT_COPY_ENGINES (default): each rank's copy engine (SDMA; over xGMI between
+ *     GPUs) copies its staging slot into the root's receive slot -- mapped by IPC handle
+ *     (exchanged with one ncclAllGather per plan) or, for ranks driven by one process, by address
+ *     -- and signals arrival with a flag in the root's memory (hipStreamWriteValue64); the root's
+ *     unpack waits on the flags (hipStreamWaitValue64) and raises per-rank slot-free flags.  No
+ *     compute unit is used for the transfer, so it runs beside a persistent render.  A world in
+ *     which some rank cannot map the root's memory falls back to RCCL transfers.
+ *   RT_COMM_TRANSPORT_RCCL: grouped ncclSend/ncclRecv on the communicator stream (the root's own
+ *     bands too: a device-local send), i.e. RCCL's transfer kernel.
+ * Loopback worlds always use the copy engines. */
+#define RT_COMM_TRANSPORT_COPY_ENGINES 0
+#define RT_COMM_TRANSPORT_RCCL 1
+int rtCommSetTransport(rt_comm comm, int transport);
+int rtCommGetTransport(rt_comm comm, int* transport, int* active);
 /* Blocking reductions of `count` doubles per local rank (values: n_local x count, in place),
  * op RT_COMM_SUM or RT_COMM_MAX; rtCommBarrier = a one-value reduction. */
 #define RT_COMM_SUM 0

@@ -99,6 +99,7 @@ class Rect(ctypes.Structure):
 
 COMM_ID_BYTES = 128
 COMM_SUM, COMM_MAX = 0, 1
+COMM_TRANSPORT_COPY_ENGINES, COMM_TRANSPORT_RCCL = 0, 1
 
 _vp = ctypes.c_void_p
 _HIP_PROTOS = {
@@ -150,6 +151,8 @@ _HIP_PROTOS = {
     "rtCommDestroy": (ctypes.c_int, [_vp]),
     "rtCommGetRank": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "rtCommShardKernel": (ctypes.c_int, [_vp, _vp]),
+    "rtCommSetTransport": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rtCommGetTransport": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "rtCommEnqueueGatherBands": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_uint,
                                                 ctypes.c_uint, ctypes.c_int, _vp]),
     "rtCommAllReduceF64": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(ctypes.c_double),

@@ -169,6 +169,16 @@ class Comm:
         check(N.hip_lib().rtCommInitLoopback(hs, n, out), "comm init loopback")
         return [cls(out[i], ctxs[i]) for i in range(n)]
 
+    def set_transport(self, transport: int) -> None:
+        """rtCommSetTransport: N.COMM_TRANSPORT_COPY_ENGINES (default) or N.COMM_TRANSPORT_RCCL."""
+        check(self._lib.rtCommSetTransport(self.handle, transport), "comm transport")
+
+    def transport(self) -> tuple[int, int]:
+        """(requested, active) transport; active -1 before the first gather."""
+        t, a = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.rtCommGetTransport(self.handle, ctypes.byref(t), ctypes.byref(a)), "comm transport")
+        return t.value, a.value
+
     def shard(self, kernel) -> None:
         """The kernel renders this rank's interleaved bands (rtCommShardKernel)."""
         check(self._lib.rtCommShardKernel(self.handle, kernel.handle), "shard kernel")

@@ -8,14 +8,25 @@
 // moves each rank's bands, packed densely, to the root:
 //
 //   context accumulation stream : [accumulate k] [pack k -> stage[s]]  [accumulate k+1] ...
-//   communicator stream         :                 (wait pack) [RCCL send/recv k]   ...
-//   root unpack stream          :                              (wait recv) [unpack k -> dst]
-//   context main stream         : [render k+1 ..........................................]
+//   communicator stream         :                 (wait pack) [transfer k -> root slot s] [flag]
+//   root unpack stream          :                      (wait flags k) [unpack k -> dst] [free s]
+//   context render streams      : [render k+1 ........................................]
 //
-// Two staging slots alternate, so step k's transfer runs under step k+1's render.  RCCL p2p
-// (grouped ncclSend/ncclRecv) lets the root receive from all peers at once on its xGMI links
-// (a ring all-gather would push N x the bytes through single links).  The packs/unpacks are 2-D
-// copies (one per rank: full bands are equally strided, plus at most one short last band).
+// Two staging slots alternate, so step k's transfer runs under step k+1's render.
+//
+// Transport (rtCommSetTransport).  A persistent render holds every CU slot until it drains, and
+// RCCL's transfer kernel (64 workgroups, 248 VGPRs, 37 KB LDS each on gfx950) fits beside it
+// nowhere: in the world-1 flow its transfer waited for renders to drain (19 ms for a 0.12-ms
+// copy) and every second step stalled on it (profiles/r04/dist_flow_ab.txt).  So by default the
+// bytes move on the COPY ENGINES (SDMA, hipMemcpyDeviceToDeviceNoCU; over xGMI between GPUs):
+// every rank copies its staging slot straight into the root's receive slot (an IPC-mapped
+// pointer to the root's memory, exchanged once per plan with one ncclAllGather), then raises its
+// arrival flag in the root's memory (hipStreamWriteValue64); the root's unpack stream waits for
+// the flags (hipStreamWaitValue64) and, after the unpack, raises each rank's slot-free flag,
+// which that rank's next copy into the slot waits for.  No compute unit is needed for the
+// transfer, no host round trip for the synchronisation.  RCCL stays for the setup, reductions
+// and barriers, and as the grouped ncclSend/ncclRecv transport (RT_COMM_TRANSPORT_RCCL; also
+// the fallback when a rank cannot map the root's memory).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -80,12 +91,12 @@ struct rt_comm_s {
     rt_context ctx = nullptr;
     ncclComm_t nc = nullptr;
     // loopback worlds (rtCommInitLoopback): no RCCL; `group` identifies the world (shared by its
-    // members) and the transfer is a device copy on the root's communicator stream
+    // members), whose gathers always run on the copy engines with the members linked by address
     const void* group = nullptr;
-    hipEvent_t xfer = nullptr;  // root: the copies of one gather done
+    hipEvent_t xfer = nullptr;  // (unused since the copy-engine transport; kept for the ABI of the struct's users)
     bool reserved = false;      // holds a CU reservation on ctx (rti::reserve_cus)
     int rank = 0, nranks = 1;
-    hipStream_t cstream = nullptr;  // RCCL
+    hipStream_t cstream = nullptr;  // transfers (copy engines or RCCL), RCCL setup and reductions
     hipStream_t ustream = nullptr;  // root: unpack
     // gather buffers for one (width, height); rebuilt when the image size changes
     unsigned W = 0, H = 0;
@@ -98,28 +109,45 @@ struct rt_comm_s {
     bool sent_valid[2] = {}, unpacked_valid[2] = {};
     int slot = 0;
     double* scratch = nullptr;  // reductions
+    // copy-engine transport (see the top of the file)
+    int transport = RT_COMM_TRANSPORT_COPY_ENGINES;  // requested (rtCommSetTransport)
+    bool ce = false;                 // this plan moves bytes on the copy engines
+    uint64_t seq = 0;                // gathers enqueued with this plan (1, 2, ...)
+    uint64_t* sflags = nullptr;      // [2] (fine-grained, this rank's memory): slot s freed by the root up to seq
+    uint64_t* rflags = nullptr;      // root, [nranks][2] (fine-grained): rank q's bytes for slot s arrived, seq
+    uint8_t* peer_parts[2] = {};     // the root's receive slots, as this rank addresses them
+    uint64_t* peer_rflags = nullptr; // the root's arrival flags, as this rank addresses them
+    std::vector<uint64_t*> peer_sflags;  // root: every rank's slot-free flags
+    std::vector<void*> ipc_opened;       // IPC mappings to close with the plan
+    // the copy-engine transfer split over streams of its own, which the runtime spreads over
+    // several SDMA engines (one engine: 61 GB/s; 2 streams 120, 8 streams 154 GB/s on MI355X,
+    // scripts/probes/gather_engines_probe.hip split, profiles/r04/gather_engines_probe.txt).
+    // Every stream shares the 4 hardware queues, though: in the world-1 flow 2 streams beat 1
+    // (0.790 vs 0.798 ms/frame) and 8 stalled the renders (1.17; profiles/r04/dist_flow_ab.txt)
+    hipStream_t xstream[8] = {};
+    hipEvent_t xgo = nullptr, xdone[8] = {};
 };
 
 namespace {
 
 // The communicator's transfer and unpack streams run at the device's greatest stream priority.
-// Two reasons, both read off a kernel trace of the world-1 flow (profiles/r04/dist_streams.txt):
+// Two reasons, both read off a kernel trace of the world-1 flow (profiles/r04/dist_flow_ab.txt):
 // * HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES 4); at normal priority these two
 //   shared the main stream's and a render stream's queue, so the next fused render sat behind the
 //   previous step's unpack, which sat behind its transfer.  High-priority streams get queues of
 //   their own.
 // * RCCL's transfer kernel needs CU slots, and a persistent render holds them all until it
-//   drains; at normal priority the next render's workgroups took the slots the draining one
-//   freed, and the transfer waited (6.4 ms for a 0.11-ms copy).  At high priority its workgroups
-//   are dispatched first.
+//   drains; at high priority its workgroups are dispatched first -- which still leaves it waiting
+//   for a drain (hence the copy-engine transport).
 #ifndef RT_COMM_STREAM_PRIO
 #define RT_COMM_STREAM_PRIO 1
 #endif
-// RCCL communicators: CUs of every XCD kept for the communicator's streams (rti::reserve_cus).
-// RCCL's transfer kernel (64 workgroups of 256 threads, 37 KB of LDS and 248 VGPRs each on
-// gfx950) does not fit beside a persistent render on any CU, so without a reservation it runs
-// only where renders drain (profiles/r04/dist_streams.txt); with one it runs at once on its own
-// CUs, and the renders lose those CUs' share (1 per XCD = 8 of 256 = 3 %).  0 = none.
+// RCCL communicators: CUs of every XCD kept for the communicator's streams (rti::reserve_cus),
+// an A/B knob of the RCCL transport.  RCCL's transfer kernel (64 workgroups of 256 threads, 37 KB
+// of LDS and 248 VGPRs each on gfx950) fits beside a persistent render on no CU; with a
+// reservation it runs at once on its own CUs, but the renders lose those CUs' share and the
+// world-1 flow measured slower than without (0.85 vs 0.82 ms/frame, profiles/r04/dist_flow_ab.txt).
+// 0 = none (default).
 int comm_events(rt_comm c, hipError_t e);
 #ifndef RT_COMM_RESERVE_PER_XCD
 #define RT_COMM_RESERVE_PER_XCD 0
@@ -144,7 +172,21 @@ int comm_streams(rt_comm c, bool rccl) {
     return comm_events(c, e);
 }
 
+#ifndef RT_COMM_XFER_STREAMS
+#define RT_COMM_XFER_STREAMS 2  // 1: the copy on the communicator stream itself
+#endif
+#ifndef RT_COMM_XFER_PRIO
+#define RT_COMM_XFER_PRIO 0     // 1: extra transfer streams at the greatest priority
+#endif
+static_assert(RT_COMM_XFER_STREAMS >= 1 && RT_COMM_XFER_STREAMS <= 8, "copy streams");
 int comm_events(rt_comm c, hipError_t e) {
+    int least = 0, greatest = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    for (int i = 0; RT_COMM_XFER_STREAMS > 1 && i < RT_COMM_XFER_STREAMS && e == hipSuccess; ++i) {
+        e = hipStreamCreateWithPriority(&c->xstream[i], hipStreamNonBlocking, RT_COMM_XFER_PRIO ? greatest : least);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xdone[i], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xgo, hipEventDisableTiming);
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipEventCreateWithFlags(&c->packed[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
@@ -156,12 +198,21 @@ int comm_events(rt_comm c, hipError_t e) {
 }
 
 void free_buffers(rt_comm c) {
+    for (void* p : c->ipc_opened) (void)hipIpcCloseMemHandle(p);
+    c->ipc_opened.clear();
     for (int s = 0; s < 2; ++s) {
         if (c->stage[s]) (void)hipFree(c->stage[s]);
         if (c->parts[s]) (void)hipFree(c->parts[s]);
         c->stage[s] = c->parts[s] = nullptr;
+        c->peer_parts[s] = nullptr;
         c->sent_valid[s] = c->unpacked_valid[s] = false;
     }
+    if (c->sflags) (void)hipFree(c->sflags);
+    if (c->rflags) (void)hipFree(c->rflags);
+    c->sflags = c->rflags = c->peer_rflags = nullptr;
+    c->peer_sflags.clear();
+    c->ce = false;
+    c->seq = 0;
     c->W = c->H = 0;
     c->root = -1;
 }
@@ -175,6 +226,12 @@ void release(rt_comm c) {
         for (hipEvent_t ev : {c->packed[s], c->sent[s], c->unpacked[s]})
             if (ev) (void)hipEventDestroy(ev);
     if (c->xfer) (void)hipEventDestroy(c->xfer);
+    for (int i = 0; i < 8; ++i) {
+        if (c->xstream[i]) (void)hipStreamSynchronize(c->xstream[i]);
+        if (c->xstream[i]) (void)hipStreamDestroy(c->xstream[i]);
+        if (c->xdone[i]) (void)hipEventDestroy(c->xdone[i]);
+    }
+    if (c->xgo) (void)hipEventDestroy(c->xgo);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -185,8 +242,10 @@ void release(rt_comm c) {
 }
 
 // buffers and plans for a W x H gather (all earlier gathers of this comm have completed)
-int ensure_plan(rt_comm c, unsigned W, unsigned H, int root) {
+int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, bool* built) {
+    *built = false;
     if (c->W == W && c->H == H && c->root == root) return RT_SUCCESS;
+    *built = true;
     (void)hipStreamSynchronize(c->cstream);
     (void)hipStreamSynchronize(c->ustream);
     (void)hipStreamSynchronize(c->ctx->astream);
@@ -201,11 +260,24 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root) {
         c->plans[q].assign(r, r + n);
     }
     c->stage_bytes = sb;
+    // copy engines: the root's receive slots and every flag word are fine-grained memory (the
+    // copies and flag writes come from other devices' engines; the unpack and the waits read
+    // them coherently), each its own allocation (an IPC handle maps a whole allocation)
+    const bool ce = c->transport == RT_COMM_TRANSPORT_COPY_ENGINES;
+    auto alloc = [&](void** p, size_t n, bool fine) {
+        return fine ? hipExtMallocWithFlags(p, n, hipDeviceMallocFinegrained) : hipMalloc(p, n);
+    };
     hipError_t e = hipSuccess;
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipMalloc(&c->stage[s], std::max<size_t>(sb, 16));
-        if (e == hipSuccess && c->rank == root) e = hipMalloc(&c->parts[s], std::max<size_t>(sb * c->nranks, 16));
+        if (e == hipSuccess && c->rank == root) e = alloc(&c->parts[s], std::max<size_t>(sb * c->nranks, 16), ce);
     }
+    if (ce && e == hipSuccess) e = alloc(reinterpret_cast<void**>(&c->sflags), 2 * sizeof(uint64_t), true);
+    if (ce && e == hipSuccess && c->rank == root)
+        e = alloc(reinterpret_cast<void**>(&c->rflags), 2 * sizeof(uint64_t) * c->nranks, true);
+    if (ce && e == hipSuccess) e = hipMemset(c->sflags, 0, 2 * sizeof(uint64_t));
+    if (ce && e == hipSuccess && c->rflags) e = hipMemset(c->rflags, 0, 2 * sizeof(uint64_t) * c->nranks);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         free_buffers(c);
         return map_hip(e);
@@ -213,6 +285,129 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root) {
     c->W = W;
     c->H = H;
     c->root = root;
+    return RT_SUCCESS;
+}
+
+// Copy-engine links of a plan whose members are all in this call (loopback worlds, and RCCL
+// worlds driven by one process): the root's slots and flags by address.  Between devices the
+// copy engines reach peer memory once peer access is on.
+int link_direct(const rt_comm* comms, int n_local, int root) {
+    rt_comm R = nullptr;
+    for (int i = 0; i < n_local; ++i)
+        if (comms[i]->rank == root) R = comms[i];
+    if (!R) return RT_INVALID_VALUE;
+    R->peer_sflags.assign(R->nranks, nullptr);
+    for (int i = 0; i < n_local; ++i) {
+        rt_comm c = comms[i];
+        if (c->ctx->device != R->ctx->device) {
+            int can = 0;
+            hipError_t e = hipDeviceCanAccessPeer(&can, c->ctx->device, R->ctx->device);
+            if (e != hipSuccess || !can) return RT_INVALID_OPERATION;
+            for (auto [a, b] : {std::pair<int, int>{c->ctx->device, R->ctx->device}, {R->ctx->device, c->ctx->device}}) {
+                (void)hipSetDevice(a);
+                e = hipDeviceEnablePeerAccess(b, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return map_hip(e);
+                (void)hipGetLastError();
+            }
+        }
+        for (int s = 0; s < 2; ++s) c->peer_parts[s] = static_cast<uint8_t*>(R->parts[s]);
+        c->peer_rflags = R->rflags;
+        R->peer_sflags[c->rank] = c->sflags;
+        c->ce = true;
+    }
+    return RT_SUCCESS;
+}
+
+// The same links across processes: every rank publishes IPC handles of its allocations (the
+// root: receive slots and arrival flags; everyone: slot-free flags) with one ncclAllGather, maps
+// the ones it needs, and the world agrees (ncclAllReduce, max) whether every rank could -- if
+// one could not, the whole world keeps the RCCL transport for this plan.
+struct IpcBlob {
+    hipIpcMemHandle_t parts[2], rflags, sflags;
+};
+int link_ipc(rt_comm c) {
+    hipError_t e = hipSetDevice(c->ctx->device);
+    IpcBlob mine{};
+    int bad = 0;
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.sflags, c->sflags);
+    if (e == hipSuccess && c->rank == c->root) {
+        e = hipIpcGetMemHandle(&mine.parts[0], c->parts[0]);
+        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.parts[1], c->parts[1]);
+        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.rflags, c->rflags);
+    }
+    if (e != hipSuccess) bad = 1;
+    std::vector<IpcBlob> all(c->nranks);
+    void* dev = nullptr;
+    const size_t nb = sizeof(IpcBlob) * (c->nranks + 1) + sizeof(int) * 2;
+    e = hipMalloc(&dev, nb);
+    if (e != hipSuccess) return map_hip(e);
+    uint8_t* d = static_cast<uint8_t*>(dev);
+    auto exchange = [&]() -> int {
+        hipError_t he = hipMemcpy(d, &mine, sizeof(mine), hipMemcpyHostToDevice);
+        if (he != hipSuccess) return map_hip(he);
+        int rc = map_nccl(ncclAllGather(d, d + sizeof(IpcBlob), sizeof(IpcBlob), ncclUint8, c->nc, c->cstream));
+        if (rc) return rc;
+        he = hipStreamSynchronize(c->cstream);
+        if (he == hipSuccess)
+            he = hipMemcpy(all.data(), d + sizeof(IpcBlob), sizeof(IpcBlob) * c->nranks, hipMemcpyDeviceToHost);
+        return map_hip(he);
+    };
+    auto open = [&](const hipIpcMemHandle_t& h, void** p) {
+        if (bad) return;
+        if (hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            bad = 1;
+            *p = nullptr;
+            return;
+        }
+        c->ipc_opened.push_back(*p);
+    };
+    int rc = exchange();
+    if (!rc) {
+        if (c->rank == c->root) {
+            c->peer_parts[0] = static_cast<uint8_t*>(c->parts[0]);
+            c->peer_parts[1] = static_cast<uint8_t*>(c->parts[1]);
+            c->peer_rflags = c->rflags;
+            c->peer_sflags.assign(c->nranks, nullptr);
+            for (int q = 0; q < c->nranks; ++q) {
+                if (q == c->rank) {
+                    c->peer_sflags[q] = c->sflags;
+                } else {
+                    void* p = nullptr;
+                    open(all[q].sflags, &p);
+                    c->peer_sflags[q] = static_cast<uint64_t*>(p);
+                }
+            }
+        } else {
+            void* p[3] = {};
+            open(all[c->root].parts[0], &p[0]);
+            open(all[c->root].parts[1], &p[1]);
+            open(all[c->root].rflags, &p[2]);
+            c->peer_parts[0] = static_cast<uint8_t*>(p[0]);
+            c->peer_parts[1] = static_cast<uint8_t*>(p[1]);
+            c->peer_rflags = static_cast<uint64_t*>(p[2]);
+        }
+        // does every rank hold its links?
+        int* flag = reinterpret_cast<int*>(d + sizeof(IpcBlob) * (c->nranks + 1));
+        hipError_t he = hipMemcpy(flag, &bad, sizeof(int), hipMemcpyHostToDevice);
+        if (he == hipSuccess) {
+            rc = map_nccl(ncclAllReduce(flag, flag + 1, 1, ncclInt32, ncclMax, c->nc, c->cstream));
+            if (!rc) he = hipStreamSynchronize(c->cstream);
+            if (!rc && he == hipSuccess) he = hipMemcpy(&bad, flag + 1, sizeof(int), hipMemcpyDeviceToHost);
+        }
+        if (!rc && he != hipSuccess) rc = map_hip(he);
+    }
+    (void)hipFree(dev);
+    if (rc) return rc;
+    if (bad) {  // the world falls back to RCCL transfers for this plan
+        for (void* p : c->ipc_opened) (void)hipIpcCloseMemHandle(p);
+        c->ipc_opened.clear();
+        c->peer_parts[0] = c->peer_parts[1] = nullptr;
+        c->peer_rflags = nullptr;
+        c->peer_sflags.clear();
+        c->ce = false;
+        return RT_SUCCESS;
+    }
+    c->ce = true;
     return RT_SUCCESS;
 }
 
@@ -234,8 +429,10 @@ hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* s
 }
 
 int rccl_transfer(const rt_comm* comms, int n_local, int root);
-int loopback_transfer(const rt_comm* comms, int n_local, int root);
 int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
+int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
+int link_direct(const rt_comm* comms, int n_local, int root);
+int link_ipc(rt_comm c);
 int check_loopback(const rt_comm* comms, int n_local);
 
 }  // namespace
@@ -365,6 +562,28 @@ int rtCommGetRank(rt_comm c, int* rank, int* nranks) {
     return RT_SUCCESS;
 }
 
+int rtCommSetTransport(rt_comm c, int transport) {
+    if (!c) return RT_INVALID_VALUE;
+    if (transport != RT_COMM_TRANSPORT_COPY_ENGINES && transport != RT_COMM_TRANSPORT_RCCL) return RT_INVALID_VALUE;
+    if (c->group && transport != RT_COMM_TRANSPORT_COPY_ENGINES) return RT_INVALID_OPERATION;
+    if (transport == c->transport) return RT_SUCCESS;
+    (void)hipSetDevice(c->ctx->device);
+    (void)hipStreamSynchronize(c->cstream);
+    (void)hipStreamSynchronize(c->ustream);
+    (void)hipStreamSynchronize(c->ctx->astream);
+    c->transport = transport;
+    free_buffers(c);  // the next gather builds the plan for it
+    return RT_SUCCESS;
+}
+
+int rtCommGetTransport(rt_comm c, int* transport, int* active) {
+    if (!c) return RT_INVALID_VALUE;
+    if (transport) *transport = c->transport;
+    // the transport the current plan uses (-1: no plan yet)
+    if (active) *active = c->W == 0 ? -1 : c->ce ? RT_COMM_TRANSPORT_COPY_ENGINES : RT_COMM_TRANSPORT_RCCL;
+    return RT_SUCCESS;
+}
+
 int rtCommShardKernel(rt_comm c, rt_kernel k) {
     if (!c) return RT_INVALID_VALUE;
     return rti::shard_kernel(k, (unsigned)c->nranks, (unsigned)c->rank);
@@ -383,14 +602,40 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
             return RT_INVALID_MEM_OBJECT;
     }
     if (int rc = check_loopback(comms, n_local)) return rc;
-    // phase 1: every rank (the root too) packs its bands on its context's accumulation stream
+    // the plans (rebuilt, by every rank alike, when the size, the root or the transport changes)
+    bool fresh = false;
+    for (int i = 0; i < n_local; ++i) {
+        hipError_t e = hipSetDevice(comms[i]->ctx->device);
+        if (e != hipSuccess) return map_hip(e);
+        bool built = false;
+        int rc = ensure_plan(comms[i], W, H, root, &built);
+        if (rc) return rc;
+        fresh |= built;
+    }
+    if (fresh && comms[0]->transport == RT_COMM_TRANSPORT_COPY_ENGINES) {
+        int rc = RT_SUCCESS;
+        if (n_local == comms[0]->nranks) {
+            rc = link_direct(comms, n_local, root);  // every member is in this call
+            if (rc && !comms[0]->group) {            // (RCCL world: keep RCCL's transfers)
+                for (int i = 0; i < n_local; ++i) comms[i]->ce = false;
+                rc = RT_SUCCESS;
+            }
+        } else if (n_local == 1 && comms[0]->nc) {
+            rc = link_ipc(comms[0]);
+        }
+        if (rc) return rc;
+    }
+    bool ce = true;
+    for (int i = 0; i < n_local; ++i) ce &= comms[i]->ce;
+    if (comms[0]->group && !ce) return RT_INVALID_OPERATION;  // a loopback world moves bytes on copy engines
+    if (ce) return ce_gather(comms, n_local, root, root_dst, outs);
+    // RCCL transport.  Phase 1: every rank (the root too) packs its bands on its context's
+    // accumulation stream
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         rt_context ctx = c->ctx;
         hipError_t e = hipSetDevice(ctx->device);
         if (e != hipSuccess) return map_hip(e);
-        int rc = ensure_plan(c, W, H, root);
-        if (rc) return rc;
         const int s = c->slot;
         uint8_t* out = static_cast<uint8_t*>(outs[i]->dptr);
         // the bands are final after every accumulation enqueued so far (astream, in order) and
@@ -411,13 +656,8 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     // several GPUs).  The root posts one receive per rank, so all its links carry data at once;
     // its own bands take the same path (a send to itself, a device-local copy) -- one uniform
     // unpack, and a world of one still runs the whole RCCL flow.
-    if (comms[0]->group) {
-        int rc = loopback_transfer(comms, n_local, root);
-        if (rc) return rc;
-    } else {
-        int rc = rccl_transfer(comms, n_local, root);
-        if (rc) return rc;
-    }
+    int rc = rccl_transfer(comms, n_local, root);
+    if (rc) return rc;
     return finish_gather(comms, n_local, root, root_dst, outs);
 }
 
@@ -442,29 +682,94 @@ int rccl_transfer(const rt_comm* comms, int n_local, int root) {
     return rc_end;
 }
 
-// loopback world: the root's communicator stream copies every rank's staging slot into its
-// receive slots (after each rank's pack), then every rank's communicator stream waits for those
-// copies -- the same stream and event chain as the RCCL send/receive above.
-int loopback_transfer(const rt_comm* comms, int n_local, int root) {
-    rt_comm R = nullptr;
-    for (int i = 0; i < n_local; ++i)
-        if (comms[i]->rank == root) R = comms[i];
-    hipError_t e = hipSetDevice(R->ctx->device);
-    for (int i = 0; i < n_local && e == hipSuccess; ++i) {
-        rt_comm c = comms[i];
-        e = hipStreamWaitEvent(R->cstream, c->packed[c->slot], 0);
+// `n` bytes on the copy engines, after and before everything on the communicator stream:
+// chunks of at least 1 MiB over the transfer streams
+hipError_t copy_engines(rt_comm c, uint8_t* dst, const uint8_t* src, size_t n) {
+    const size_t k = std::max<size_t>(1, std::min<size_t>(RT_COMM_XFER_STREAMS, n >> 20));
+    if (k == 1) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->cstream);
+    const size_t chunk = ((n + k - 1) / k + 255) & ~(size_t)255;
+    hipError_t e = hipEventRecord(c->xgo, c->cstream);
+    for (size_t i = 0; i < k && e == hipSuccess; ++i) {
+        const size_t off = i * chunk;
+        if (off >= n) break;
+        e = hipStreamWaitEvent(c->xstream[i], c->xgo, 0);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(static_cast<uint8_t*>(R->parts[R->slot]) + (size_t)c->rank * R->stage_bytes,
-                               c->stage[c->slot], c->stage_bytes, hipMemcpyDeviceToDevice, R->cstream);
+            e = hipMemcpyAsync(dst + off, src + off, std::min(chunk, n - off), hipMemcpyDeviceToDeviceNoCU,
+                               c->xstream[i]);
+        if (e == hipSuccess) e = hipEventRecord(c->xdone[i], c->xstream[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->xdone[i], 0);
     }
-    if (e == hipSuccess) e = hipEventRecord(R->xfer, R->cstream);
-    for (int i = 0; i < n_local && e == hipSuccess; ++i) {
+    return e;
+}
+
+// Copy-engine gather (see the top of the file).  Flags carry the gather's sequence number seq
+// (1, 2, ... within a plan): rflags[q][s] = seq when rank q's bytes for slot s have landed in the
+// root's receive slot, sflags[s] = seq when the root has unpacked slot s -- the next copy into
+// that slot (gather seq + 2) waits for it.  Gathering into the root's own output, its own bands
+// are in place: it neither packs nor sends them.
+int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs) {
+    for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
-        if (c == R) continue;
-        e = hipSetDevice(c->ctx->device);
-        if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, R->xfer, 0);
+        rt_context ctx = c->ctx;
+        const int s = c->slot;
+        const uint64_t seq = ++c->seq;
+        const bool into_out = c->rank == root && (!root_dst || root_dst == outs[i]);
+        hipError_t e = hipSetDevice(ctx->device);
+        if (e == hipSuccess && !into_out) {
+            // pack on the accumulation stream, after the accumulations (and main-stream work)
+            // that write `out`, once the copy engine has read the slot's previous contents
+            e = rti::main_tail_wait(ctx, ctx->astream);
+            if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);
+            if (e == hipSuccess)
+                e = copy_rects(c->plans[c->rank], static_cast<uint8_t*>(outs[i]->dptr),
+                               static_cast<uint8_t*>(c->stage[s]), true, ctx->astream);
+            if (e == hipSuccess) e = hipEventRecord(c->packed[s], ctx->astream);
+            if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
+            if (e == hipSuccess) ctx->apending = true;
+            // transfer on the communicator stream: into the root's slot once the root has
+            // unpacked what the slot held two gathers ago, then the arrival flag
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->packed[s], 0);
+            if (e == hipSuccess && seq > 2)
+                e = hipStreamWaitValue64(c->cstream, c->sflags + s, seq - 2, hipStreamWaitValueGte, ~0ull);
+            if (e == hipSuccess) e = copy_engines(c, c->peer_parts[s] + (size_t)c->rank * c->stage_bytes,
+                                                  static_cast<const uint8_t*>(c->stage[s]), c->stage_bytes);
+            if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank + s, seq, 0);
+            if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
+            if (e == hipSuccess) c->sent_valid[s] = true;
+        }
+        if (e != hipSuccess) return map_hip(e);
     }
-    return map_hip(e);
+    for (int i = 0; i < n_local; ++i) {
+        rt_comm c = comms[i];
+        rt_context ctx = c->ctx;
+        const int s = c->slot;
+        const uint64_t seq = c->seq;
+        hipError_t e = hipSetDevice(ctx->device);
+        hipStream_t tail = c->cstream;
+        if (e == hipSuccess && c->rank == root) {
+            // the root: wait for every sender's bytes, unpack them, free the slot for each sender
+            const bool into_out = !root_dst || root_dst == outs[i];
+            uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
+            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+                if (!(into_out && q == c->rank))
+                    e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q + s, seq, hipStreamWaitValueGte, ~0ull);
+            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+                if (!(into_out && q == c->rank))
+                    e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
+                                   false, c->ustream);
+            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+                if (!(into_out && q == c->rank)) e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q] + s, seq, 0);
+            if (e == hipSuccess) e = hipEventRecord(c->unpacked[s], c->ustream);
+            if (e == hipSuccess) c->unpacked_valid[s] = true;
+            tail = c->ustream;
+        }
+        // reads on this context wait for its part of the gather (qs)
+        if (e == hipSuccess) e = hipEventRecord(ctx->gtail, tail);
+        if (e != hipSuccess) return map_hip(e);
+        ctx->gpending = true;
+        c->slot ^= 1;
+    }
+    return RT_SUCCESS;
 }
 
 // phase 3: the root unpacks every rank's bands into the destination
@@ -484,7 +789,7 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
             // it.  (An unpack that the next accumulation had to wait for chained that
             // accumulation, and the render after it, to the transfer: RCCL's kernel gets CUs only
             // as a persistent render drains, so every second render started a step late --
-            // world-1 0.90 vs 0.77 ms/frame, profiles/r04/dist_streams.txt.)  Reads of the
+            // world-1 0.90 vs 0.77 ms/frame, profiles/r04/dist_flow_ab.txt.)  Reads of the
             // image wait for it through the context's queue (gtail, qs()).
             const bool into_out = !root_dst || root_dst == outs[i];
             uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);

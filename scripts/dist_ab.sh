@@ -7,8 +7,9 @@
 #   DIST_LIBS="main nocu ..."        a subset of the builds
 #   DIST_ENVS="name:VAR=v,VAR2=w ..."  extra runs of the main build under environment settings
 #                                      (e.g. RCCL's channel counts), named name
+#   DIST_TAG=tag                       outputs under gpurun_out/dist_ab_tag
 set -u
-OUT=gpurun_out/dist_ab
+OUT=gpurun_out/dist_ab${DIST_TAG:+_$DIST_TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
 reps=${1:-2}; shift || true

@@ -5,7 +5,7 @@
 //  3. two processes on the one GPU: the child opens the parent's buffers by IPC handle, copies
 //     its bytes into them with a no-CU copy and raises a flag there (hipStreamWriteValue64); the
 //     parent's stream waits for the flag (hipStreamWaitValue64) and checks the bytes.
-// usage: gather_engines_probe   (prints one line per measurement; exits non-zero on a mismatch)
+// usage: gather_engines_probe [ipc|split]   (prints one line per measurement; exits non-zero on a mismatch)
 // The processes fork before either touches the GPU.
 #include <hip/hip_runtime.h>
 #include <signal.h>
@@ -162,7 +162,13 @@ static int two_processes() {
     void* B;
     uint64_t* flag;
     CK(hipMalloc(&B, kBytes));
-    CK(hipMalloc(&flag, 64));
+    // the flag word as fine-grained device memory when the runtime exports it by IPC (else plain)
+    const bool fine = getenv("PROBE_FINE") != nullptr;
+    if (fine)
+        CK(hipExtMallocWithFlags((void**)&flag, 64, hipDeviceMallocFinegrained));
+    else
+        CK(hipMalloc(&flag, 64));
+    printf("parent: flag memory %s\n", fine ? "fine-grained" : "hipMalloc");
     CK(hipMemset(B, 0, kBytes));
     CK(hipMemset(flag, 0, 64));
     CK(hipDeviceSynchronize());
@@ -173,7 +179,8 @@ static int two_processes() {
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     // the wait is queued before the child has even started copying
     CK(hipStreamWaitValue64(s, flag, 1, hipStreamWaitValueGte, ~0ull));
-    uint32_t* host = (uint32_t*)malloc(kBytes);
+    uint32_t* host = nullptr;
+    CK(hipHostMalloc((void**)&host, kBytes, 0));
     CK(hipMemcpyAsync(host, B, kBytes, hipMemcpyDeviceToHost, s));
     if (write(to_child[1], &hb, sizeof(hb)) != sizeof(hb) || write(to_child[1], &hf, sizeof(hf)) != sizeof(hf)) return 4;
     CK(hipStreamSynchronize(s));
@@ -188,7 +195,44 @@ static int two_processes() {
     return bad ? 1 : (WIFEXITED(st) ? WEXITSTATUS(st) : 7);
 }
 
+// 4. one 132.7-MB no-CU copy split into k chunks on k streams: do the streams reach k engines?
+static int split_copies() {
+    CK(hipSetDevice(0));
+    void *A, *B;
+    CK(hipMalloc(&A, kBytes));
+    CK(hipMalloc(&B, kBytes));
+    hipStream_t st[16];
+    for (int i = 0; i < 16; ++i) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    hipEvent_t e0, e1, ev[16];
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 16; ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    for (int k : {1, 2, 4, 8, 16}) {
+        float best = 1e9f;
+        for (int rep = 0; rep < 3; ++rep) {
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, st[0]));
+            const size_t chunk = (kBytes / k + 255) & ~(size_t)255;
+            for (int i = 0; i < k; ++i) {
+                if (i) CK(hipStreamWaitEvent(st[i], e0, 0));
+                const size_t off = chunk * i, n = off >= kBytes ? 0 : (off + chunk > kBytes ? kBytes - off : chunk);
+                if (n) CK(hipMemcpyAsync((char*)B + off, (char*)A + off, n, hipMemcpyDeviceToDeviceNoCU, st[i]));
+                if (i) {
+                    CK(hipEventRecord(ev[i], st[i]));
+                    CK(hipStreamWaitEvent(st[0], ev[i], 0));
+                }
+            }
+            CK(hipEventRecord(e1, st[0]));
+            CK(hipEventSynchronize(e1));
+            best = fminf(best, ms_between(e0, e1));
+        }
+        printf("no-CU copy in %2d chunks on %2d streams: %.3f ms (%.1f GB/s)\n", k, k, best, kBytes / (best * 1e-3) / 1e9);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && !strcmp(argv[1], "ipc")) return two_processes();
+    if (argc > 1 && !strcmp(argv[1], "split")) return split_copies();
     return single_process();
 }

@@ -103,8 +103,9 @@ def _read(ctx, buf, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["copy", "rccl"])
 @pytest.mark.parametrize("init,into_out", [("rank", False), ("rank", True), ("all", False)])
-def test_gather_world_of_one(cornell, init, into_out):
+def test_gather_world_of_one(cornell, init, into_out, transport):
     import clrt
     W, H = 640, 360
     ctx = clrt.CLContext(0)
@@ -113,16 +114,20 @@ def test_gather_world_of_one(cornell, init, into_out):
     else:
         (comm,) = mg.Comm.init_all([ctx])
     assert (comm.rank, comm.nranks) == (0, 1)
+    want = N.COMM_TRANSPORT_RCCL if transport == "rccl" else N.COMM_TRANSPORT_COPY_ENGINES
+    comm.set_transport(want)
+    assert comm.transport() == (want, -1)
     bufs, out, k = _setup(ctx, cornell, W, H)
     comm.shard(k)
     dst = None if into_out else ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
     images = []
-    for step in range(3):  # pipelined: gathers queued behind back-to-back fused renders
+    for step in range(5):  # pipelined: gathers queued behind back-to-back fused renders (slots reused)
         k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
         ctx.ExecuteKernelFrames(k, W * H, 8)
         mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=dst)
         if step == 0:
             images.append(_read(ctx, dst or out, W * H))
+            assert comm.transport() == (want, want)
     ctx.Finish()
     gathered = _read(ctx, dst or out, W * H)
     rendered = _read(ctx, out, W * H)
@@ -162,6 +167,31 @@ def test_gather_after_per_frame_launches(cornell):
 
 
 @pytest.mark.gpu
+def test_gather_plan_rebuilt_on_size_and_transport_change(cornell):
+    """A new image size (or transport) rebuilds the plan -- flags and sequence numbers start over
+    -- between pipelined gathers of the old one; every gathered image equals its render."""
+    import clrt
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    for (W, H), transport in (((256, 144), 0), ((200, 120), 0), ((200, 120), 1), ((256, 144), 0)):
+        comm.set_transport(transport)
+        bufs, out, k = _setup(ctx, cornell, W, H)
+        comm.shard(k)
+        dst = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+        for step in range(4):
+            k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+            ctx.ExecuteKernelFrames(k, W * H, 8)
+            mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=dst)
+        assert _read(ctx, dst, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+        assert comm.transport() == (transport, transport)
+        for b in bufs + [out, dst]:
+            b.release()
+        k.release()
+    comm.destroy()
+    ctx.release()
+
+
+@pytest.mark.gpu
 def test_allreduce_and_barrier_world_of_one():
     import clrt
     ctx = clrt.CLContext(0)
@@ -174,14 +204,17 @@ def test_allreduce_and_barrier_world_of_one():
 
 
 @pytest.mark.gpu
-def test_bench_rccl_flow_world_of_one(tmp_path):
+@pytest.mark.parametrize("transport", ["copy", "rccl"])
+def test_bench_rccl_flow_world_of_one(tmp_path, transport):
     """bench.py's N > 1 flow (file rendezvous, RCCL communicator, sharded fused renders, the
-    pipelined gather every step, max-over-ranks timing) at WORLD_SIZE 1; --check-gather makes
-    rank 0 re-render the frame unsharded and compare the gathered image byte for byte."""
+    pipelined gather every step into the root's image buffer, max-over-ranks timing) at
+    WORLD_SIZE 1, on either transport; --check-gather makes rank 0 re-render the frame unsharded
+    and compare the gathered image byte for byte."""
     env = dict(os.environ, RT_COMM_ID_FILE=str(tmp_path / "comm.id"))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--force-dist", "--check-gather",
+                        "--transport", transport,
                         "--width", "1280", "--height", "720", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -190,10 +223,11 @@ def test_bench_rccl_flow_world_of_one(tmp_path):
 
 # ---- N > 1 on one GPU: the loopback world (rtCommInitLoopback) ----------------------------------
 # The same sharding, pack on the accumulation stream, two-slot pipelining, per-rank receive slots
-# parts[s] + q*stage_bytes, per-rank unpack plans (with the short last band) and event chain
-# across ranks as the RCCL world -- only the grouped ncclSend/ncclRecv is replaced by device
-# copies.  Every rank is its own context on the one GPU of the test box.  (The RCCL transfer for
-# N > 1 itself needs N GPUs: the driver's 8-GPU bench.)
+# parts[s] + q*stage_bytes, per-rank unpack plans (with the short last band) and the copy-engine
+# transport's flag protocol (arrival flags in the root's memory, slot-free flags in each rank's)
+# as a multi-GPU world -- only the ranks' links are addresses in this process instead of IPC
+# mappings.  Every rank is its own context on the one GPU of the test box.  (Copies between GPUs
+# over xGMI need N GPUs: the driver's 8-GPU bench.)
 def _scene(cornell, name):
     if name == "cornell":
         return cornell
