@@ -96,9 +96,10 @@ def parse():
                    help="N>1: wait for each step's gather before queueing the next step (no pipelining)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the N>1 flow (RCCL communicator + gather) even at WORLD_SIZE 1")
-    p.add_argument("--transport", choices=["copy", "rccl"], default="copy",
+    p.add_argument("--transport", choices=["copy", "rccl", "copy-ipc"], default="copy",
                    help="N>1: how the gather moves the bands (rtCommSetTransport): copy engines over xGMI "
-                        "(default) or RCCL send/recv kernels")
+                        "(default), RCCL send/recv kernels, or copy engines linked by IPC handles even at "
+                        "world size 1 (the multi-process path)")
     p.add_argument("--check-gather", action="store_true",
                    help="after timing, rank 0 renders the whole frame unsharded and checks the gathered "
                         "image against it byte for byte")
@@ -342,7 +343,8 @@ def main():
     # whole data path (pack, transfer, unpack)
     img = None
     if comm is not None:
-        comm.set_transport(N.COMM_TRANSPORT_RCCL if args.transport == "rccl" else N.COMM_TRANSPORT_COPY_ENGINES)
+        comm.set_transport({"rccl": N.COMM_TRANSPORT_RCCL, "copy": N.COMM_TRANSPORT_COPY_ENGINES,
+                            "copy-ipc": N.COMM_TRANSPORT_COPY_ENGINES_IPC}[args.transport])
         if rank == 0:
             img = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16)
 

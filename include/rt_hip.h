@@ -382,9 +382,14 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
  *     which some rank cannot map the root's memory falls back to RCCL transfers.
  *   RT_COMM_TRANSPORT_RCCL: grouped ncclSend/ncclRecv on the communicator stream (the root's own
  *     bands too: a device-local send), i.e. RCCL's transfer kernel.
+ *   RT_COMM_TRANSPORT_COPY_ENGINES_IPC: the copy engines with the links always set up the
+ *     multi-process way (IPC handles through ncclAllGather, a world-wide ncclAllReduce on the
+ *     outcome) even when every rank is driven by this process -- the one-process-per-GPU path,
+ *     selectable at any world size (one local communicator per call).
  * Loopback worlds always use the copy engines. */
 #define RT_COMM_TRANSPORT_COPY_ENGINES 0
 #define RT_COMM_TRANSPORT_RCCL 1
+#define RT_COMM_TRANSPORT_COPY_ENGINES_IPC 2
 int rtCommSetTransport(rt_comm comm, int transport);
 int rtCommGetTransport(rt_comm comm, int* transport, int* active);
 /* Blocking reductions of `count` doubles per local rank (values: n_local x count, in place),

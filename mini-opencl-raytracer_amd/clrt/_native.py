@@ -99,7 +99,7 @@ class Rect(ctypes.Structure):
 
 COMM_ID_BYTES = 128
 COMM_SUM, COMM_MAX = 0, 1
-COMM_TRANSPORT_COPY_ENGINES, COMM_TRANSPORT_RCCL = 0, 1
+COMM_TRANSPORT_COPY_ENGINES, COMM_TRANSPORT_RCCL, COMM_TRANSPORT_COPY_ENGINES_IPC = 0, 1, 2
 
 _vp = ctypes.c_void_p
 _HIP_PROTOS = {

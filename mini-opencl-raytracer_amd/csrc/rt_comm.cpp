@@ -112,6 +112,7 @@ struct rt_comm_s {
     // copy-engine transport (see the top of the file)
     int transport = RT_COMM_TRANSPORT_COPY_ENGINES;  // requested (rtCommSetTransport)
     bool ce = false;                 // this plan moves bytes on the copy engines
+    bool ipc_linked = false;         // ... with its links exchanged as IPC handles (link_ipc)
     uint64_t seq = 0;                // gathers enqueued with this plan (1, 2, ...)
     uint64_t* sflags = nullptr;      // [2] (fine-grained, this rank's memory): slot s freed by the root up to seq
     uint64_t* rflags = nullptr;      // root, [nranks][2] (fine-grained): rank q's bytes for slot s arrived, seq
@@ -176,7 +177,7 @@ int comm_streams(rt_comm c, bool rccl) {
 #define RT_COMM_XFER_STREAMS 2  // 1: the copy on the communicator stream itself
 #endif
 #ifndef RT_COMM_XFER_PRIO
-#define RT_COMM_XFER_PRIO 0     // 1: extra transfer streams at the greatest priority
+#define RT_COMM_XFER_PRIO 1     // extra transfer streams at the greatest priority (own hardware queues)
 #endif
 static_assert(RT_COMM_XFER_STREAMS >= 1 && RT_COMM_XFER_STREAMS <= 8, "copy streams");
 int comm_events(rt_comm c, hipError_t e) {
@@ -211,7 +212,7 @@ void free_buffers(rt_comm c) {
     if (c->rflags) (void)hipFree(c->rflags);
     c->sflags = c->rflags = c->peer_rflags = nullptr;
     c->peer_sflags.clear();
-    c->ce = false;
+    c->ce = c->ipc_linked = false;
     c->seq = 0;
     c->W = c->H = 0;
     c->root = -1;
@@ -263,7 +264,7 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, bool* built) {
     // copy engines: the root's receive slots and every flag word are fine-grained memory (the
     // copies and flag writes come from other devices' engines; the unpack and the waits read
     // them coherently), each its own allocation (an IPC handle maps a whole allocation)
-    const bool ce = c->transport == RT_COMM_TRANSPORT_COPY_ENGINES;
+    const bool ce = c->transport != RT_COMM_TRANSPORT_RCCL;
     auto alloc = [&](void** p, size_t n, bool fine) {
         return fine ? hipExtMallocWithFlags(p, n, hipDeviceMallocFinegrained) : hipMalloc(p, n);
     };
@@ -407,7 +408,7 @@ int link_ipc(rt_comm c) {
         c->ce = false;
         return RT_SUCCESS;
     }
-    c->ce = true;
+    c->ce = c->ipc_linked = true;
     return RT_SUCCESS;
 }
 
@@ -564,7 +565,9 @@ int rtCommGetRank(rt_comm c, int* rank, int* nranks) {
 
 int rtCommSetTransport(rt_comm c, int transport) {
     if (!c) return RT_INVALID_VALUE;
-    if (transport != RT_COMM_TRANSPORT_COPY_ENGINES && transport != RT_COMM_TRANSPORT_RCCL) return RT_INVALID_VALUE;
+    if (transport != RT_COMM_TRANSPORT_COPY_ENGINES && transport != RT_COMM_TRANSPORT_RCCL &&
+        transport != RT_COMM_TRANSPORT_COPY_ENGINES_IPC)
+        return RT_INVALID_VALUE;
     if (c->group && transport != RT_COMM_TRANSPORT_COPY_ENGINES) return RT_INVALID_OPERATION;
     if (transport == c->transport) return RT_SUCCESS;
     (void)hipSetDevice(c->ctx->device);
@@ -580,7 +583,8 @@ int rtCommGetTransport(rt_comm c, int* transport, int* active) {
     if (!c) return RT_INVALID_VALUE;
     if (transport) *transport = c->transport;
     // the transport the current plan uses (-1: no plan yet)
-    if (active) *active = c->W == 0 ? -1 : c->ce ? RT_COMM_TRANSPORT_COPY_ENGINES : RT_COMM_TRANSPORT_RCCL;
+    if (active) *active = c->W == 0 ? -1 : !c->ce ? RT_COMM_TRANSPORT_RCCL : c->ipc_linked ? RT_COMM_TRANSPORT_COPY_ENGINES_IPC
+                                                                                   : RT_COMM_TRANSPORT_COPY_ENGINES;
     return RT_SUCCESS;
 }
 
@@ -612,9 +616,12 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         if (rc) return rc;
         fresh |= built;
     }
-    if (fresh && comms[0]->transport == RT_COMM_TRANSPORT_COPY_ENGINES) {
+    if (fresh && comms[0]->transport != RT_COMM_TRANSPORT_RCCL) {
         int rc = RT_SUCCESS;
-        if (n_local == comms[0]->nranks) {
+        if (comms[0]->transport == RT_COMM_TRANSPORT_COPY_ENGINES_IPC) {
+            if (n_local != 1 || !comms[0]->nc) return RT_INVALID_OPERATION;
+            rc = link_ipc(comms[0]);
+        } else if (n_local == comms[0]->nranks) {
             rc = link_direct(comms, n_local, root);  // every member is in this call
             if (rc && !comms[0]->group) {            // (RCCL world: keep RCCL's transfers)
                 for (int i = 0; i < n_local; ++i) comms[i]->ce = false;
@@ -683,9 +690,11 @@ int rccl_transfer(const rt_comm* comms, int n_local, int root) {
 }
 
 // `n` bytes on the copy engines, after and before everything on the communicator stream:
-// chunks of at least 1 MiB over the transfer streams
+// chunks of at least 1 MiB over the transfer streams (several ranks driven by one process share
+// its hardware queues, so they copy on the one stream)
 hipError_t copy_engines(rt_comm c, uint8_t* dst, const uint8_t* src, size_t n) {
-    const size_t k = std::max<size_t>(1, std::min<size_t>(RT_COMM_XFER_STREAMS, n >> 20));
+    const bool shared = !c->ipc_linked && c->nranks > 1;
+    const size_t k = shared ? 1 : std::max<size_t>(1, std::min<size_t>(RT_COMM_XFER_STREAMS, n >> 20));
     if (k == 1) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->cstream);
     const size_t chunk = ((n + k - 1) / k + 255) & ~(size_t)255;
     hipError_t e = hipEventRecord(c->xgo, c->cstream);
@@ -702,12 +711,18 @@ hipError_t copy_engines(rt_comm c, uint8_t* dst, const uint8_t* src, size_t n) {
     return e;
 }
 
-// Copy-engine gather (see the top of the file).  Flags carry the gather's sequence number seq
-// (1, 2, ... within a plan): rflags[q][s] = seq when rank q's bytes for slot s have landed in the
-// root's receive slot, sflags[s] = seq when the root has unpacked slot s -- the next copy into
-// that slot (gather seq + 2) waits for it.  Gathering into the root's own output, its own bands
-// are in place: it neither packs nor sends them.
+// Copy-engine gather (see the top of the file).  Between processes (IPC links), flags carry the
+// gather's sequence number seq (1, 2, ... within a plan): rflags[q][s] = seq when rank q's bytes
+// for slot s have landed in the root's receive slot, sflags[s] = seq when the root has unpacked
+// slot s -- the next copy into that slot (gather seq + 2) waits for it.  Ranks driven by this
+// process (loopback worlds, rtCommInitAll) order the same steps with events instead (the
+// sender's `sent`, the root's `unpacked`): no waiting kernel on a hardware queue their other
+// streams share.  Gathering into the root's own output, its own bands are in place: it neither
+// packs nor sends them.
 int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs) {
+    rt_comm R = nullptr;  // the root, when it is driven by this call
+    for (int i = 0; i < n_local; ++i)
+        if (comms[i]->rank == root) R = comms[i];
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         rt_context ctx = c->ctx;
@@ -729,11 +744,16 @@ int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, cons
             // transfer on the communicator stream: into the root's slot once the root has
             // unpacked what the slot held two gathers ago, then the arrival flag
             if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->packed[s], 0);
-            if (e == hipSuccess && seq > 2)
-                e = hipStreamWaitValue64(c->cstream, c->sflags + s, seq - 2, hipStreamWaitValueGte, ~0ull);
+            if (c->ipc_linked) {
+                if (e == hipSuccess && seq > 2)
+                    e = hipStreamWaitValue64(c->cstream, c->sflags + s, seq - 2, hipStreamWaitValueGte, ~0ull);
+            } else if (e == hipSuccess && R->unpacked_valid[s]) {
+                e = hipStreamWaitEvent(c->cstream, R->unpacked[s], 0);
+            }
             if (e == hipSuccess) e = copy_engines(c, c->peer_parts[s] + (size_t)c->rank * c->stage_bytes,
                                                   static_cast<const uint8_t*>(c->stage[s]), c->stage_bytes);
-            if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank + s, seq, 0);
+            if (e == hipSuccess && c->ipc_linked)
+                e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank + s, seq, 0);
             if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
             if (e == hipSuccess) c->sent_valid[s] = true;
         }
@@ -750,14 +770,19 @@ int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, cons
             // the root: wait for every sender's bytes, unpack them, free the slot for each sender
             const bool into_out = !root_dst || root_dst == outs[i];
             uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
-            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-                if (!(into_out && q == c->rank))
-                    e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q + s, seq, hipStreamWaitValueGte, ~0ull);
+            if (c->ipc_linked) {
+                for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+                    if (!(into_out && q == c->rank))
+                        e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q + s, seq, hipStreamWaitValueGte, ~0ull);
+            } else {
+                for (int j = 0; j < n_local && e == hipSuccess; ++j)
+                    if (!(into_out && comms[j] == c)) e = hipStreamWaitEvent(c->ustream, comms[j]->sent[s], 0);
+            }
             for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
                 if (!(into_out && q == c->rank))
                     e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
                                    false, c->ustream);
-            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+            for (int q = 0; c->ipc_linked && q < c->nranks && e == hipSuccess; ++q)
                 if (!(into_out && q == c->rank)) e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q] + s, seq, 0);
             if (e == hipSuccess) e = hipEventRecord(c->unpacked[s], c->ustream);
             if (e == hipSuccess) c->unpacked_valid[s] = true;

@@ -5,13 +5,14 @@ after another.  Prints per-rank ms per 8-frame step and the strong-scaling effic
 T1 / (N * max_r T_r).
 
 RT_EMU_GATHER=1 adds the gather bench.py runs every step (rtCommEnqueueGatherBands): rank r's
-context joins a loopback world of N contexts on this GPU (rtCommInitLoopback: the RCCL world's
-pack on the accumulation stream, two staging slots, per-rank receive slots, unpack on the root's
-stream; the RCCL transfer replaced by device copies) in which only rank r renders; every step
-all N ranks pack and root 0 unpacks every other rank's bands into its own output, pipelined with
-the next step as in bench.py.  The idle ranks' packs and the root's unpack run on this GPU too,
-so a non-root rank's time includes copies its GPU would not make (~0.1 GB per step at 4K): an
-upper bound.  What the loopback world cannot show is RCCL's own transfer kernel between GPUs.
+context joins a loopback world of N contexts on this GPU (rtCommInitLoopback: pack on the
+accumulation stream, two staging slots, copy-engine transfer into the root's receive slots,
+unpack on the root's stream) in which only rank r renders; every step all N ranks pack and copy
+and root 0 unpacks every other rank's bands into its own output, pipelined with the next step as
+in bench.py.  All N ranks' copies then share THIS GPU's copy engines (N x 16.6 MB per 4K step at
+N = 8, ~2.2 ms at 61 GB/s), where each real rank copies only its own share on its own engines:
+with the copy-engine transport this measures one GPU's engines, not a rank's step -- a loose
+upper bound (profiles/r04/rank_emulation_r04.txt).
 
 usage: rank_emulation.py [N ...]   (env: RT_EMU_MATH, RT_EMU_SCENE=cornell|bunny, RT_EMU_STEPS,
        RT_EMU_FUSED=1: the 8 frames as one rtEnqueueKernelFrames call (default 1),

@@ -103,9 +103,11 @@ def _read(ctx, buf, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["copy", "rccl"])
+@pytest.mark.parametrize("transport", ["copy", "rccl", "copy-ipc"])
 @pytest.mark.parametrize("init,into_out", [("rank", False), ("rank", True), ("all", False)])
 def test_gather_world_of_one(cornell, init, into_out, transport):
+    if transport == "copy-ipc" and init == "all":
+        pytest.skip("the IPC links are the one-process-per-GPU setup's")
     import clrt
     W, H = 640, 360
     ctx = clrt.CLContext(0)
@@ -114,7 +116,8 @@ def test_gather_world_of_one(cornell, init, into_out, transport):
     else:
         (comm,) = mg.Comm.init_all([ctx])
     assert (comm.rank, comm.nranks) == (0, 1)
-    want = N.COMM_TRANSPORT_RCCL if transport == "rccl" else N.COMM_TRANSPORT_COPY_ENGINES
+    want = {"rccl": N.COMM_TRANSPORT_RCCL, "copy": N.COMM_TRANSPORT_COPY_ENGINES,
+            "copy-ipc": N.COMM_TRANSPORT_COPY_ENGINES_IPC}[transport]
     comm.set_transport(want)
     assert comm.transport() == (want, -1)
     bufs, out, k = _setup(ctx, cornell, W, H)
@@ -204,7 +207,7 @@ def test_allreduce_and_barrier_world_of_one():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["copy", "rccl"])
+@pytest.mark.parametrize("transport", ["copy", "rccl", "copy-ipc"])
 def test_bench_rccl_flow_world_of_one(tmp_path, transport):
     """bench.py's N > 1 flow (file rendezvous, RCCL communicator, sharded fused renders, the
     pipelined gather every step into the root's image buffer, max-over-ranks timing) at
