@@ -1002,7 +1002,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end
-    a.flagTiles = fused && !wf && si == RT_SCHED_STEP && lds && RT_RAY_RING ? 1u : 0u;
+    a.flagTiles = fused && !wf && si == RT_SCHED_STEP && ((lds && RT_RAY_RING) || (goct && RT_STEAL && RT_GOCT_TILE_FLAGS)) ? 1u
+                  : fused && !wf && si == RT_SCHED_STEP && goct && RT_GOCT_NOFLAGS ? 2u : 0u;
     a.specWalk = k->spec_walk && k->nested ? 1u : 0u;
 
     const int mi = k->math;

@@ -46,8 +46,11 @@ struct KernelArgs {
     // launch; radiance per (frame slot, gid) in radBuf[slot * radStride + gid] (null: one frame)
     float4* radBuf;
     // primary-miss flags: 1 = radiance (K_rad x3), not in radBuf.  flagTiles 0: one byte per
-    // [slot * radStride + gid]; flagTiles 1 (renders that generate camera rays a whole 8x8 tile at
-    // a time, the ray ring): one 64-bit word per [slot * nTiles + tile], bit = pixel's lane in the tile
+    // [slot * radStride + gid]; flagTiles 1 (the LDS walk's ray ring, and -- RT_GOCT_TILE_FLAGS --
+    // the HBM/L2 octant walk, which hands out each tile's work items from one wave): one 64-bit
+    // word per [slot * nTiles + tile], bit = pixel's lane in the tile, written once by the wave
+    // that handed the tile out; every path not decided at its camera ray stores its radiance.
+    // flagTiles 2 (the HBM/L2 octant walk, RT_GOCT_NOFLAGS): no flags, every path stores it
     uint8_t* frameFlags;
     uint32_t flagTiles;
     uint32_t nFrames, radStride;
@@ -81,6 +84,15 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 // per wave), from which its siblings take single tiles once the work counter is dry
 #ifndef RT_STEAL
 #define RT_STEAL 1
+#endif
+// fused HBM/L2 octant walks: primary misses decided at refill, flags as one 64-bit word per
+// (frame, tile) (step_body, kGoctTiles); 0 = a flag byte per path
+#ifndef RT_GOCT_TILE_FLAGS
+#define RT_GOCT_TILE_FLAGS 0
+#endif
+// fused HBM/L2 octant walks: no flags at all -- every path stores its radiance (flagTiles 2)
+#ifndef RT_GOCT_NOFLAGS
+#define RT_GOCT_NOFLAGS 1
 #endif
 constexpr uint32_t kStealBytes = RT_STEAL ? 4u * 8u + 32u : 0u;  // (padded to whole float4s)
 

@@ -896,6 +896,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // instructions, that walk's binding resource -- bunny proxy +12 %, profiles/r04/spec_walk.txt)
     constexpr bool kSpec = RT_SPEC && kLdsScene && !kGlobalOct && (!kStats || RT_SPEC_STATS);
     uint32_t pend = 0u;  // (kSpec) pending leaf code count << 24 | first while >= kLeafMin
+    // fused HBM/L2 octant walks (a.flagTiles): camera rays that miss the root box are decided at
+    // refill, as the ray ring does for LDS scenes, and each tile's primary-miss flags go out as one
+    // 64-bit word when its wave has handed out the tile's last work item (tile_sky accumulates
+    // them): no flag byte per path.  A byte per path, merged in L2 from scattered stores, left as
+    // 32-B partial-line writes: 0.45 of the bunny launch's 1.49 GB (profiles/r04/goct_flags.txt)
+    // (measured 1 % slower on the bunny proxy than the byte flags: the root visit at refill costs
+    // load instructions outside the node bursts -- off, RT_GOCT_TILE_FLAGS)
+    const bool kGoctTiles = RT_GOCT_TILE_FLAGS && kGlobalOct && RT_STEAL && fused && a.flagTiles == 1u;
+    // fused HBM/L2 octant walks without flags (a.flagTiles 2, the default there): every path
+    // stores its radiance, primary misses included, and the accumulation reads every frame -- the
+    // flag byte per path is gone (0.45 GB of 32-B partial-line writes per bunny launch)
+    const bool kNoFlags = kGlobalOct && fused && a.flagTiles == 2u;
+    [[maybe_unused]] unsigned long long tile_sky = 0ull;  // wave-uniform
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
@@ -935,8 +948,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     // (ray ring: the tile's flags were written when it was generated -- a
                     // path that still ends as K_rad stores its radiance like any other, which
                     // the accumulation reads to the same bits)
-                    if (!skyv || kRing) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
-                    if (!kRing) a.frameFlags[gid] = skyv ? 1u : 0u;
+                    if (!skyv || kRing || kGoctTiles || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
+                    if (!kRing && !kGoctTiles && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
             }
@@ -1133,22 +1146,22 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), 64u - used);  // within one 8x8 tile
+                // fused work order: frame-major (all tiles of a frame, then the next: cheap sky
+                // tiles and costly tiles mix in every wave), or -- large launches on scenes read
+                // from HBM/L2 (a.tileMajor) -- tile-major, a tile's frames back to back for
+                // coherent node and triangle fetches (profiles/r01/work_order_ab.txt)
+                uint32_t tile = unit >> 6;  // wave-uniform (scalar division)
+                uint32_t slot = 0;
+                if (fused && a.tileMajor) {
+                    slot = tile % a.nFrames;
+                    tile /= a.nFrames;
+                } else if (fused) {
+                    slot = tile / a.nTiles;
+                    tile -= slot * a.nTiles;
+                }
+                bool sky = false;
                 if (state == kIdle && rank < take) {
                     const uint32_t w = used + rank;  // chunks are whole 8x8 tiles
-                    uint32_t tile = unit >> 6;  // wave-uniform (scalar division)
-                    // fused work order: frame-major (all tiles of a frame, then the next: cheap
-                    // sky tiles and costly tiles mix in every wave), or -- large launches on
-                    // scenes read from HBM/L2 (a.tileMajor) -- tile-major, a tile's frames back
-                    // to back for coherent node and triangle fetches
-                    // (profiles/r01/work_order_ab.txt)
-                    uint32_t slot = 0;
-                    if (fused && a.tileMajor) {
-                        slot = tile % a.nFrames;
-                        tile /= a.nFrames;
-                    } else if (fused) {
-                        slot = tile / a.nTiles;
-                        tile -= slot * a.nTiles;
-                    }
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
                     const uint32_t x = tx * 8u + (w & 7u),
                                    row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
@@ -1166,7 +1179,28 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                             cur = 0;
-                                if (kStats) ++st.rays;
+                            if (kStats) ++st.rays;
+                            if (kGoctTiles) {
+                                // the walk's first visit (the root, t = kMaxDist) made here: a miss
+                                // is a primary miss (Intersect finds nothing, the bounce adds the
+                                // sky and breaks, Render returns K_rad: kernel_bvh.cl:358-361,
+                                // :383) -- flagged, no path; a hit continues at the root's successor
+                                if (kStats) ++st.visits;
+                                uint32_t sk;
+                                const uint32_t nx = oct_step<kBofs>(sc, a, 0u, ray, kMaxDist, sk);
+                                if (nx == a.nNodes) {
+                                    sky = true;
+                                    state = kIdle;
+                                    cur = kNotWalking;
+                                    if (a.hitIds && last_frame) {
+                                        a.hitIds[(uint32_t)g64] = -1;
+                                        a.hitT[(uint32_t)g64] = kMaxDist;
+                                    }
+                                } else {
+                                    cur = nx;
+                                    leaf_i = sk;
+                                }
+                            }
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
                             if (a.hitIds && last_frame) {
@@ -1177,6 +1211,18 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                 }
 #if RT_STEAL
+                if (kGoctTiles) {
+                    // this round's primary misses into the tile's word: bit (used + rank) per lane
+                    unsigned long long b = sky ? 1ull << (used + rank) : 0ull;
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off, 64);
+                    tile_sky |= b;
+                    if (used + take >= 64u) {  // the tile's last work item handed out
+                        if (lane == 0)
+                            reinterpret_cast<unsigned long long*>(a.frameFlags)[(size_t)slot * a.nTiles + tile] = tile_sky;
+                        tile_sky = 0ull;
+                    }
+                }
                 tile_used += take;
 #else
                 chunk_used += take;
@@ -1577,7 +1623,7 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (live) {
             if (a.frameCount != 0u) o = a.result[gid];
-            fl = a.flagTiles ? load_tile_flags(a, tile, lane) : load_flags(a, gid);
+            fl = a.flagTiles == 1u ? load_tile_flags(a, tile, lane) : a.flagTiles == 2u ? 0u : load_flags(a, gid);
             sky = fl == (1u << a.nFrames) - 1u &&
                   (a.frameCount == 0u ||
                    (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold));
