@@ -293,6 +293,17 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   PERFRAME_DEFER_MIN                work items from which PERFRAME_DEFER 2 defers (default 4 Mi)
  *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
  *                                     as many as fit, default; fewer = fewer waves per SIMD)
+ *   PERFRAME_BATCH                    step schedule: rtEnqueueKernel calls of this kernel queued
+ *                                     back to back with consecutive frameCount and otherwise equal
+ *                                     arguments (FRAME_SEED aside: KernelEntry never reads it) are
+ *                                     coalesced into one fused launch of up to this many frames
+ *                                     (1..8, default 8; 1 = every call launches).  The launch is
+ *                                     made before any other call touches the context -- a read, a
+ *                                     write, rtFinish, another launch, a kernel setting, a release
+ *                                     -- so results are the same bits at every point the host can
+ *                                     observe; kernels with stats or timing on are not coalesced.
+ *                                     An error of a coalesced launch is returned by the next call
+ *                                     on the context that returns one (rtFinish at the latest).
  *   SPEC_WALK                         step schedule, LDS octant walk, builds with the speculative
  *                                     walk compiled in (RT_SPEC=1; the shipped build has it out,
  *                                     measured slower): 1 (default) = speculative walk (a lane
@@ -320,7 +331,8 @@ enum rt_tuning {
     RT_TUNE_PERFRAME_DEFER = 19,
     RT_TUNE_MAX_BLOCKS = 20,
     RT_TUNE_PERFRAME_DEFER_MIN = 21,
-    RT_TUNE_SPEC_WALK = 22
+    RT_TUNE_SPEC_WALK = 22,
+    RT_TUNE_PERFRAME_BATCH = 23
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);
 int rtKernelGetTuning(rt_kernel k, int param, int* value);

@@ -77,6 +77,7 @@ struct rt_kernel_s {
     int pf_defer = 2;                  // per-frame step launches through radiance slots + accumulation
                                        // (0 never, 1 always, 2 while the previous one still runs)
     uint32_t pf_defer_min = 4u << 20;  // ... (2) from this many work items per launch
+    uint32_t pf_batch = rtk::kMaxFusedFrames;  // RT_TUNE_PERFRAME_BATCH: frames coalesced per launch
     int max_blocks = 0;                // persistent grid: workgroups per CU (0 = as many as fit)
     int global_oct = 1;                // scenes not in LDS: walk octant records in HBM/L2 (step;
                                        // bunny proxy 1.80 -> 1.58 ms/frame, profiles/r02/goct_sweep.txt)
@@ -145,6 +146,34 @@ int ensure_device(rt_context ctx) {
     if (!ctx) return RT_INVALID_CONTEXT;
     return map_hip(hipSetDevice(ctx->device));
 }
+
+// an error of an earlier coalesced launch (rti::flush_frames), else rc
+int pending_error(rt_context ctx, int rc) {
+    if (ctx && ctx->pend_error != RT_SUCCESS) {
+        const int e = ctx->pend_error;
+        ctx->pend_error = RT_SUCCESS;
+        return e;
+    }
+    return rc;
+}
+
+// the context's coalesced frames, when they are `k`'s (a setting of k is about to change how
+// they would launch)
+void flush_kernel(rt_kernel k) {
+    if (k && k->ctx && k->ctx->pend_k == k) (void)rti::flush_frames(k->ctx);
+}
+
+// the arguments a coalesced launch compares (FRAME_COUNT continues the run; FRAME_SEED is never
+// read by KernelEntry, kernel_bvh.cl:415-456)
+bool same_args(const rt_context ctx, const rt_kernel k) {
+    for (int i = RT_ARG_WIDTH; i < RT_ARG_COUNT; ++i) {
+        if (i == RT_ARG_FRAME_COUNT || i == RT_ARG_FRAME_SEED || i >= RT_ARG_CAMERA_POS) continue;
+        if (ctx->pend_u32[i] != k->u32[i]) return false;
+    }
+    if (std::memcmp(ctx->pend_f3, k->f3, sizeof(k->f3)) != 0) return false;
+    return std::memcmp(ctx->pend_bufs, k->bufs, sizeof(k->bufs)) == 0;
+}
+
 
 // Host view of a buffer's bytes (shadow, or a device read-back).
 int host_bytes(rt_mem m, std::vector<uint8_t>& tmp, const uint8_t** out) {
@@ -720,6 +749,7 @@ int rtReleaseKernel(rt_kernel k) {
     if (!k) return RT_INVALID_KERNEL;
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
+    flush_kernel(k);
     (void)hipStreamSynchronize(qs(k->ctx));
     for (auto* list : {&k->pending_events, &k->pending_accum})
         for (auto& pr : *list) {
@@ -774,12 +804,89 @@ int rtSetKernelArg(rt_kernel k, unsigned index, size_t size, const void* value) 
 
 static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_t n_frames);
 
+
+}  // extern "C"
+
+int rti::flush_frames(rt_context ctx) {
+    if (!ctx || !ctx->pend_k) return RT_SUCCESS;
+    rt_kernel k = ctx->pend_k;
+    ctx->pend_k = nullptr;  // (enqueue's own qs() calls find nothing pending)
+    // launch with the arguments the frames were enqueued with, then give the kernel back its own
+    uint32_t u32[RT_ARG_COUNT];
+    float f3[3][4];
+    rt_mem bufs[4];
+    std::memcpy(u32, k->u32, sizeof(u32));
+    std::memcpy(f3, k->f3, sizeof(f3));
+    std::memcpy(bufs, k->bufs, sizeof(bufs));
+    std::memcpy(k->u32, ctx->pend_u32, sizeof(u32));
+    std::memcpy(k->f3, ctx->pend_f3, sizeof(f3));
+    std::memcpy(k->bufs, ctx->pend_bufs, sizeof(bufs));
+    std::memcpy(&k->u32[RT_ARG_FRAME_COUNT], &ctx->pend_f0, 4);
+    const int rc = enqueue(ctx, k, ctx->pend_gws, ctx->pend_n);
+    std::memcpy(k->u32, u32, sizeof(u32));
+    std::memcpy(k->f3, f3, sizeof(f3));
+    std::memcpy(k->bufs, bufs, sizeof(bufs));
+    if (rc != RT_SUCCESS && ctx->pend_error == RT_SUCCESS) ctx->pend_error = rc;
+    return rc;
+}
+
+extern "C" {
+
+// Frame coalescing (RT_TUNE_PERFRAME_BATCH).  The reference's host issues one ExecuteKernel per
+// frame (CLRaytracer.cpp:52-55); a host that queues frames without looking at them in between
+// gets them as fused launches (rtEnqueueKernelFrames: bit-identical to the per-frame launches,
+// test_fused_frames.py), one launch tail per run instead of one per frame.  The frame is checked
+// here as a launch would check it, so argument and scene errors still come back from this call.
 int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
-    return enqueue(ctx, k, global_work_size, 1);
+    const bool coalesce = ctx && k && k->ctx == ctx && k->pf_batch > 1 && k->sched == RT_SCHED_STEP && !k->stats &&
+                          !k->timing;
+    if (!coalesce) {
+        if (ctx && ctx->pend_k) {
+            const int rc = rti::flush_frames(ctx);
+            if (rc) return pending_error(ctx, rc);
+        }
+        return enqueue(ctx, k, global_work_size, 1);
+    }
+    int rc = ensure_device(ctx);
+    if (rc) return rc;
+    for (int i = 0; i < RT_ARG_COUNT; ++i)
+        if (!k->set[i]) return RT_INVALID_KERNEL_ARGS;
+    if (global_work_size == 0 || global_work_size > 0xffffffffull) return RT_INVALID_GLOBAL_WORK_SIZE;
+    uint32_t W, H, f;
+    std::memcpy(&W, &k->u32[RT_ARG_WIDTH], 4);
+    std::memcpy(&H, &k->u32[RT_ARG_HEIGHT], 4);
+    std::memcpy(&f, &k->u32[RT_ARG_FRAME_COUNT], 4);
+    if (W == 0 || H == 0) return RT_INVALID_KERNEL_ARGS;
+    if (k->bufs[RT_ARG_BUFFER_OUT]->size < global_work_size * 16) return RT_INVALID_GLOBAL_WORK_SIZE;
+    if (k->hit_ids && (k->hit_ids->size < (global_work_size + kHitPad) * 4 || k->hit_t->size < global_work_size * 4))
+        return RT_INVALID_MEM_OBJECT;
+    if (ctx->pend_k == k && ctx->pend_gws == global_work_size && ctx->pend_n < k->pf_batch &&
+        f == ctx->pend_f0 + ctx->pend_n && f != 0u && same_args(ctx, k)) {
+        ++ctx->pend_n;  // the next frame of the run
+        return pending_error(ctx, RT_SUCCESS);
+    }
+    if (ctx->pend_k) {
+        rc = rti::flush_frames(ctx);
+        if (rc) return pending_error(ctx, rc);
+    }
+    rc = prepare_scene(k);  // (a malformed scene is refused now, not at the launch)
+    if (rc) return rc;
+    ctx->pend_k = k;
+    ctx->pend_gws = global_work_size;
+    ctx->pend_f0 = f;
+    ctx->pend_n = 1;
+    std::memcpy(ctx->pend_u32, k->u32, sizeof(k->u32));
+    std::memcpy(ctx->pend_f3, k->f3, sizeof(k->f3));
+    std::memcpy(ctx->pend_bufs, k->bufs, sizeof(k->bufs));
+    return pending_error(ctx, RT_SUCCESS);
 }
 
 int rtEnqueueKernelFrames(rt_context ctx, rt_kernel k, size_t global_work_size, unsigned n_frames) {
     if (n_frames == 0) return RT_INVALID_VALUE;
+    if (ctx && ctx->pend_k) {
+        const int rc = rti::flush_frames(ctx);
+        if (rc) return pending_error(ctx, rc);
+    }
     if (n_frames == 1 || !k || (k->sched != RT_SCHED_STEP && k->sched != RT_SCHED_WAVEFRONT)) {
         // one launch per frame (the other schedules have no fused form): same results
         if (!k) return RT_INVALID_KERNEL;
@@ -1238,7 +1345,7 @@ int rtEnqueueReadBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, s
     hipError_t e = hipMemcpyAsync(dst, static_cast<uint8_t*>(m->dptr) + offset, size,
                                   hipMemcpyDeviceToHost, qs(ctx));
     if (e == hipSuccess && blocking) e = host_wait(ctx);
-    return map_hip(e);
+    return pending_error(ctx, map_hip(e));
 }
 
 int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, size_t size,
@@ -1252,7 +1359,7 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, 
     hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(m->dptr) + offset, src, size,
                                   hipMemcpyHostToDevice, qs(ctx));
     if (e == hipSuccess && blocking) e = host_wait(ctx);
-    return map_hip(e);
+    return pending_error(ctx, map_hip(e));
 }
 
 int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem m, size_t offset, size_t size, void* dst) {
@@ -1267,11 +1374,12 @@ int rtEnqueueCopyBufferToPointer(rt_context ctx, rt_mem m, size_t offset, size_t
 int rtFinish(rt_context ctx) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
-    return map_hip(host_wait(ctx));
+    return pending_error(ctx, map_hip(host_wait(ctx)));
 }
 
 int rtKernelSetMathMode(rt_kernel k, int mode) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     if (mode != RT_MATH_PINNED && mode != RT_MATH_DEVICELIB && mode != RT_MATH_SHIPPED) return RT_INVALID_VALUE;
     k->math = mode;
     return RT_SUCCESS;
@@ -1279,6 +1387,7 @@ int rtKernelSetMathMode(rt_kernel k, int mode) {
 
 int rtKernelSetSchedule(rt_kernel k, int sched) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     if (sched != RT_SCHED_TILES && sched != RT_SCHED_STEP &&
         sched != RT_SCHED_WAVEFRONT)
         return RT_INVALID_VALUE;
@@ -1288,6 +1397,7 @@ int rtKernelSetSchedule(rt_kernel k, int sched) {
 
 int rtKernelSetRowInterleave(rt_kernel k, unsigned period, unsigned phase) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     if (period == 0 || phase >= period) return RT_INVALID_VALUE;
     k->band_period = period;
     k->band_phase = phase;
@@ -1300,6 +1410,7 @@ int rtKernelSetRowInterleave(rt_kernel k, unsigned period, unsigned phase) {
 // rtCommShardKernel: the gather's band plan counts bands from image row 0, the kernel from the
 // first row of its work range -- so a comm-sharded kernel renders whole frames only
 int rti::shard_kernel(rt_kernel k, unsigned period, unsigned phase) {
+    flush_kernel(k);
     if (!k) return RT_INVALID_KERNEL;
     if (k->range_first != 0 || k->range_last != 0) return RT_INVALID_OPERATION;
     int rc = rtKernelSetRowInterleave(k, period, phase);
@@ -1313,6 +1424,7 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
                                      size_t width_bytes, size_t rows, void* dst, size_t dst_pitch) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     if (!src || src->ctx != ctx || !dst) return RT_INVALID_MEM_OBJECT;
     if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
@@ -1341,6 +1453,7 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
 int rtContextSetReadbackOnAccumStream(rt_context ctx, int enable) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     ctx->readback_on_astream = enable != 0;
     return RT_SUCCESS;
 }
@@ -1349,6 +1462,7 @@ int rtContextGetAccumStream(rt_context ctx, void** s) {
     if (!ctx) return RT_INVALID_CONTEXT;
     if (!s) return RT_INVALID_VALUE;
     if (!ctx->overlap) ctx->mexposed = true;  // the main stream leaves the library's view
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     *s = ctx->overlap ? ctx->astream : qs(ctx);
     return RT_SUCCESS;
 }
@@ -1357,6 +1471,7 @@ int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src
                                      size_t dst_offset, size_t dst_pitch, size_t width_bytes, size_t rows) {
     int rc = ensure_device(ctx);
     if (rc) return rc;
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     if (!dst || dst->ctx != ctx || !src) return RT_INVALID_MEM_OBJECT;
     if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
@@ -1367,6 +1482,7 @@ int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src
 
 int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     if (last != 0 && last < first) return RT_INVALID_VALUE;
     if (k->comm_sharded && (first != 0 || last != 0)) return RT_INVALID_OPERATION;
     k->range_first = first;
@@ -1376,6 +1492,7 @@ int rtKernelSetWorkRange(rt_kernel k, uint64_t first, uint64_t last) {
 
 int rtKernelSetHitBuffers(rt_kernel k, rt_mem ids, rt_mem t) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     if ((ids == nullptr) != (t == nullptr)) return RT_INVALID_MEM_OBJECT;
     if (ids && (ids->ctx != k->ctx || t->ctx != k->ctx)) return RT_INVALID_MEM_OBJECT;
     k->hit_ids = ids;
@@ -1385,18 +1502,21 @@ int rtKernelSetHitBuffers(rt_kernel k, rt_mem ids, rt_mem t) {
 
 int rtKernelSetStats(rt_kernel k, int enable) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     k->stats = enable != 0;
     return RT_SUCCESS;
 }
 
 int rtKernelSetTiming(rt_kernel k, int enable) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     k->timing = enable != 0;
     return RT_SUCCESS;
 }
 
 int rtKernelGetStats(rt_kernel k, rt_stats* out) {
     if (!k || !out) return RT_INVALID_VALUE;
+    flush_kernel(k);
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
     unsigned long long h[kStatWords] = {};
@@ -1423,6 +1543,7 @@ int rtKernelGetStats(rt_kernel k, rt_stats* out) {
 
 int rtKernelResetStats(rt_kernel k) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     int rc = ensure_device(k->ctx);
     if (rc) return rc;
     rc = drain_events(k);
@@ -1444,12 +1565,14 @@ int rtKernelGetSceneInLDS(rt_kernel k, int* in_lds) {
 
 int rtKernelForceGlobalScene(rt_kernel k, int force) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     k->force_global = force != 0;
     return RT_SUCCESS;
 }
 
 int rtBufferGetDevicePointer(rt_mem m, void** dptr) {
     if (!m || !dptr) return RT_INVALID_VALUE;
+    if (m->ctx && m->ctx->pend_k) (void)rti::flush_frames(m->ctx);  // the caller may touch the bytes
     *dptr = m->dptr;
     return RT_SUCCESS;
 }
@@ -1525,6 +1648,7 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth) 
 
 int rtKernelSetTuning(rt_kernel k, int param, int value) {
     if (!k) return RT_INVALID_KERNEL;
+    flush_kernel(k);
     auto in = [&](int lo, int hi) { return value >= lo && value <= hi; };
     switch (param) {
         case RT_TUNE_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min = (uint32_t)value; break;
@@ -1553,6 +1677,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_PERFRAME_DEFER: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_defer = value; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: if (value < 0) return RT_INVALID_VALUE; k->pf_defer_min = (uint32_t)value; break;
         case RT_TUNE_SPEC_WALK: if (!in(0, 1)) return RT_INVALID_VALUE; k->spec_walk = value; break;
+        case RT_TUNE_PERFRAME_BATCH: if (!in(1, (int)rtk::kMaxFusedFrames)) return RT_INVALID_VALUE; k->pf_batch = (uint32_t)value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1582,6 +1707,7 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: *value = (int)k->pf_defer_min; break;
         case RT_TUNE_SPEC_WALK: *value = k->spec_walk; break;
+        case RT_TUNE_PERFRAME_BATCH: *value = (int)k->pf_batch; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;

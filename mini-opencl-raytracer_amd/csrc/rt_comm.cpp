@@ -606,6 +606,8 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
             return RT_INVALID_MEM_OBJECT;
     }
     if (int rc = check_loopback(comms, n_local)) return rc;
+    for (int i = 0; i < n_local; ++i)  // coalesced per-frame launches first: the gather reads their output
+        if (comms[i]->ctx->pend_k) (void)rti::flush_frames(comms[i]->ctx);
     // the plans (rebuilt, by every rank alike, when the size, the root or the transport changes)
     bool fresh = false;
     for (int i = 0; i < n_local; ++i) {

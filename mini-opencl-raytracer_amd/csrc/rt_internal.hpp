@@ -58,6 +58,17 @@ struct rt_context_s {
     // the accumulations, so reads of the gathered image are ordered after it
     hipEvent_t gtail = nullptr;
     bool gpending = false;
+    // per-frame launches queued back to back and not launched yet (rt_capi.cpp, frame
+    // coalescing): frames pend_f0 .. pend_f0 + pend_n - 1 of pend_k with the arguments they were
+    // enqueued with; launched as one fused launch before anything else touches the context
+    // (flush_frames; qs() flushes, so every enqueue, read, write and wait does)
+    rt_kernel pend_k = nullptr;
+    size_t pend_gws = 0;
+    uint32_t pend_f0 = 0, pend_n = 0;
+    uint32_t pend_u32[RT_ARG_COUNT] = {};
+    float pend_f3[3][4] = {};
+    rt_mem pend_bufs[4] = {};
+    int pend_error = RT_SUCCESS;  // a failed coalesced launch, reported by the next call that can
 };
 
 struct rt_mem_s {
@@ -83,8 +94,14 @@ inline int map_hip(hipError_t e) {
     }
 }
 
-// The context's stream, after every pending accumulation and gather (see rt_context_s).
+// Launch the coalesced per-frame launches of `ctx`, if any (rt_capi.cpp).  Returns their error,
+// which is also kept in ctx->pend_error for the next call that reports one.
+int flush_frames(rt_context ctx);
+
+// The context's stream, after every pending accumulation and gather (see rt_context_s) and the
+// coalesced per-frame launches.
 inline hipStream_t qs(rt_context ctx) {
+    if (ctx->pend_k) (void)flush_frames(ctx);
     if (ctx->apending) {
         (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
         ctx->apending = false;
