@@ -1307,6 +1307,7 @@ int rtBuildBVHEx(rt_context ctx, rt_mem tris, size_t n_tris, unsigned max_prims_
     if (method != RT_BVH_LBVH && method != RT_BVH_PLOC) return RT_INVALID_VALUE;
     int rc = ensure_device(ctx);
     if (rc) return rc;
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     if (!tris || !nodes || tris->ctx != ctx || nodes->ctx != ctx) return RT_INVALID_MEM_OBJECT;
     if (!n_nodes || n_tris == 0 || n_tris >= (1u << 30)) return RT_INVALID_VALUE;
     if (tris->size < n_tris * sizeof(rt_cl_triangle)) return RT_INVALID_BUFFER_SIZE;
@@ -1354,6 +1355,8 @@ int rtEnqueueWriteBuffer(rt_context ctx, rt_mem m, int blocking, size_t offset, 
     if (rc) return rc;
     if (!m || m->ctx != ctx) return RT_INVALID_MEM_OBJECT;
     if (!src || offset > m->size || size > m->size - offset) return RT_INVALID_VALUE;
+    // coalesced frames launch first, reading (and packing) the scene as it was
+    if (ctx->pend_k) (void)rti::flush_frames(ctx);
     if (m->shadow_valid) std::memcpy(m->shadow.data() + offset, src, size);
     ++m->generation;
     hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(m->dptr) + offset, src, size,
@@ -1476,6 +1479,8 @@ int rtEnqueueCopyPointerRectToBuffer(rt_context ctx, const void* src, size_t src
     if (rows == 0 || width_bytes == 0) return RT_SUCCESS;
     if (width_bytes > src_pitch || width_bytes > dst_pitch) return RT_INVALID_VALUE;
     if (dst_offset + (rows - 1) * dst_pitch + width_bytes > dst->size) return RT_INVALID_VALUE;
+    dst->shadow_valid = false;  // device contents change: a scene buffer is re-read and repacked
+    ++dst->generation;
     return map_hip(hipMemcpy2DAsync(static_cast<uint8_t*>(dst->dptr) + dst_offset, dst_pitch, src, src_pitch,
                                     width_bytes, rows, hipMemcpyDeviceToDevice, qs(ctx)));
 }
