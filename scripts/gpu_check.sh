@@ -58,7 +58,6 @@ for step in "$@"; do
                    done
                    for sc in cornell bunny; do
                      RT_EMU_SCENE=$sc run rank_emulation_$sc 600 python scripts/rank_emulation.py
-                     RT_EMU_SCENE=$sc RT_EMU_GATHER=1 run rank_emulation_gather_$sc 900 python scripts/rank_emulation.py 1 8
                    done ;;
     configs) run cfg3_default 600 python bench.py && \
              run cfg3_pinned 300 python bench.py --math pinned --no-cpu-baseline && \
