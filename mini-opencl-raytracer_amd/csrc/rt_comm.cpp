@@ -32,7 +32,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -326,6 +328,64 @@ int link_direct(const rt_comm* comms, int n_local, int root) {
 struct IpcBlob {
     hipIpcMemHandle_t parts[2], rflags, sflags;
 };
+
+// the host waits for `s` until `deadline` (no hang: a stream stuck on a flag is reported)
+bool wait_until(hipStream_t s, std::chrono::steady_clock::time_point deadline) {
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady || std::chrono::steady_clock::now() > deadline) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// reads `n` u64 words of device memory until every word equals `v` or the deadline passes
+bool poll_words(const uint64_t* dev, size_t n, size_t stride, uint64_t v, std::chrono::steady_clock::time_point deadline) {
+    std::vector<uint64_t> h(n * stride);
+    for (;;) {
+        if (hipMemcpy(h.data(), dev, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return false;
+        bool all = true;
+        for (size_t i = 0; i < n; ++i) all &= h[i * stride] == v;
+        if (all) return true;
+        if (std::chrono::steady_clock::now() > deadline) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// One trial round over fresh IPC links: every rank copies a 4-KB pattern into its part of the
+// root's slot 0 on the copy engines and raises its arrival flag; the root waits for every flag,
+// checks every pattern, raises every rank's slot-free flag; each rank waits for its own; all
+// flags go back to 0.  Returns 1 when anything failed or timed out.
+int ipc_handshake(rt_comm c) {
+    constexpr uint64_t kMagic = 0x52545f4c494e4b31ull;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(20);
+    const size_t n = std::min<size_t>(c->stage_bytes, 4096);
+    hipError_t e = hipMemsetAsync(c->stage[0], (c->rank + 1) & 0xff, n, c->cstream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(c->peer_parts[0] + (size_t)c->rank * c->stage_bytes, c->stage[0], n,
+                           hipMemcpyDeviceToDeviceNoCU, c->cstream);
+    if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank, kMagic, 0);
+    if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
+    if (c->rank == c->root) {
+        if (!poll_words(c->rflags, (size_t)c->nranks, 2, kMagic, deadline)) return 1;
+        std::vector<uint8_t> got(n);
+        for (int q = 0; q < c->nranks; ++q) {
+            if (hipMemcpy(got.data(), static_cast<uint8_t*>(c->parts[0]) + (size_t)q * c->stage_bytes, n,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+                return 1;
+            for (uint8_t b : got)
+                if (b != (uint8_t)((q + 1) & 0xff)) return 1;
+        }
+        for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+            e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q], kMagic, 0);
+        if (e == hipSuccess) e = hipMemsetAsync(c->rflags, 0, 2 * sizeof(uint64_t) * c->nranks, c->ustream);
+        if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
+    }
+    if (!poll_words(c->sflags, 1, 1, kMagic, deadline)) return 1;
+    e = hipMemset(c->sflags, 0, 2 * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e == hipSuccess ? 0 : 1;
+}
 int link_ipc(rt_comm c) {
     hipError_t e = hipSetDevice(c->ctx->device);
     IpcBlob mine{};
@@ -388,6 +448,20 @@ int link_ipc(rt_comm c) {
             c->peer_rflags = static_cast<uint64_t*>(p[2]);
         }
         // does every rank hold its links?
+        int* flag = reinterpret_cast<int*>(d + sizeof(IpcBlob) * (c->nranks + 1));
+        hipError_t he = hipMemcpy(flag, &bad, sizeof(int), hipMemcpyHostToDevice);
+        if (he == hipSuccess) {
+            rc = map_nccl(ncclAllReduce(flag, flag + 1, 1, ncclInt32, ncclMax, c->nc, c->cstream));
+            if (!rc) he = hipStreamSynchronize(c->cstream);
+            if (!rc && he == hipSuccess) he = hipMemcpy(&bad, flag + 1, sizeof(int), hipMemcpyDeviceToHost);
+        }
+        if (!rc && he != hipSuccess) rc = map_hip(he);
+    }
+    // the links hold: one small transfer and both flags across the world, polled from the host
+    // with a deadline, before any gather relies on them (a world whose first real gather waited on
+    // a flag that never arrives would hang instead of falling back)
+    if (!rc && !bad) {
+        bad = ipc_handshake(c);
         int* flag = reinterpret_cast<int*>(d + sizeof(IpcBlob) * (c->nranks + 1));
         hipError_t he = hipMemcpy(flag, &bad, sizeof(int), hipMemcpyHostToDevice);
         if (he == hipSuccess) {
