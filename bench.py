@@ -234,9 +234,10 @@ def cpu_baseline(scene, args, rays_per_step):
 
 def drop_in(r, args, rays_per_step, steps=3):
     """The drop-in path beside the fused headline: the same step as the reference's RenderFrame
-    loop issues it -- one rtEnqueueKernel (ExecuteKernel) per frame -- (a) queued back to back,
+    loop issues it -- one rtEnqueueKernel (ExecuteKernel) per frame -- (a) queued back to back for
+    `steps` steps (the library coalesces queued frames into fused launches, RT_TUNE_PERFRAME_BATCH),
     (b) with RenderFrame's per-frame ReadBuffer of the W*H*16-B image + Finish (CLRaytracer.cpp:
-    57-59; PCIe read-back inside, so never the headline)."""
+    57-59; PCIe read-back inside, so never the headline), one step."""
     k = make_kernel(r.ctx, r.bufs, r.out, args)
     W, H, F = args.width, args.height, args.frames
 
@@ -447,7 +448,7 @@ def main():
     if check:
         line["check_gather"] = check
     if world == 1 and comm is None and args.launch == "fused" and not args.no_drop_in:
-        line["drop_in"] = drop_in(r, args, rays_per_step)
+        line["drop_in"] = drop_in(r, args, rays_per_step, steps=args.steps)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(scene, args, pinned_rays(r, args))
     print(json.dumps(line))
