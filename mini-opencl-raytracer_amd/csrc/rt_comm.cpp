@@ -353,9 +353,10 @@ bool poll_words(const uint64_t* dev, size_t n, size_t stride, uint64_t v, std::c
 }
 
 // One trial round over fresh IPC links: every rank copies a 4-KB pattern into its part of the
-// root's slot 0 on the copy engines and raises its arrival flag; the root waits for every flag,
-// checks every pattern, raises every rank's slot-free flag; each rank waits for its own; all
-// flags go back to 0.  Returns 1 when anything failed or timed out.
+// root's slot 0 on the copy engines and raises its arrival flag; the root waits for every flag
+// (from the host, then -- once they are in memory -- with the stream waits gathers use), checks
+// every pattern, raises every rank's slot-free flag; each rank waits for its own the same two
+// ways; all flags go back to 0.  Returns 1 when anything failed or timed out.
 int ipc_handshake(rt_comm c) {
     constexpr uint64_t kMagic = 0x52545f4c494e4b31ull;
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(20);
@@ -368,6 +369,10 @@ int ipc_handshake(rt_comm c) {
     if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
     if (c->rank == c->root) {
         if (!poll_words(c->rflags, (size_t)c->nranks, 2, kMagic, deadline)) return 1;
+        // the flags are in memory; the unpack stream's waits must see them too (the production path)
+        for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+            e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q, kMagic, hipStreamWaitValueGte, ~0ull);
+        if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
         std::vector<uint8_t> got(n);
         for (int q = 0; q < c->nranks; ++q) {
             if (hipMemcpy(got.data(), static_cast<uint8_t*>(c->parts[0]) + (size_t)q * c->stage_bytes, n,
@@ -382,6 +387,8 @@ int ipc_handshake(rt_comm c) {
         if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
     }
     if (!poll_words(c->sflags, 1, 1, kMagic, deadline)) return 1;
+    e = hipStreamWaitValue64(c->cstream, c->sflags, kMagic, hipStreamWaitValueGte, ~0ull);
+    if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
     e = hipMemset(c->sflags, 0, 2 * sizeof(uint64_t));
     if (e == hipSuccess) e = hipDeviceSynchronize();
     return e == hipSuccess ? 0 : 1;
