@@ -192,6 +192,47 @@ void soups() {
 
 }  // namespace
 
+// Checkpoint files (rtiSaveAccum / rtiLoadAccum): a round trip, header-only reads, and every
+// damaged form -- truncated at each length, one flipped byte anywhere, a wrong size -- refused
+// without a read past the buffer or the file.
+void checkpoints() {
+    const unsigned W = 5, H = 3;
+    std::vector<float> px(4 * W * H), back(4 * W * H);
+    for (size_t i = 0; i < px.size(); ++i) px[i] = (float)i * 0.25f - 3.0f;
+    const std::string path = g_dir + "/accum.bin";
+    if (rtiSaveAccum(path.c_str(), px.data(), W, H, 9) != RT_SUCCESS) std::abort();
+    unsigned w = 0, h = 0, f = 0;
+    if (rtiLoadAccum(path.c_str(), nullptr, &w, &h, &f) != RT_SUCCESS || w != W || h != H || f != 9) std::abort();
+    if (rtiLoadAccum(path.c_str(), back.data(), &w, &h, &f) != RT_SUCCESS || back != px) std::abort();
+    std::FILE* in = std::fopen(path.c_str(), "rb");
+    std::vector<unsigned char> bytes;
+    for (int c; (c = std::fgetc(in)) != EOF;) bytes.push_back((unsigned char)c);
+    std::fclose(in);
+    const std::string bad = g_dir + "/accum_bad.bin";
+    auto write = [&](const std::vector<unsigned char>& b) {
+        std::FILE* o = std::fopen(bad.c_str(), "wb");
+        if (!b.empty()) std::fwrite(b.data(), 1, b.size(), o);
+        std::fclose(o);
+    };
+    for (size_t n = 0; n < bytes.size(); ++n) {  // truncated
+        write(std::vector<unsigned char>(bytes.begin(), bytes.begin() + n));
+        if (rtiLoadAccum(bad.c_str(), back.data(), &w, &h, &f) == RT_SUCCESS) std::abort();
+        ++g_rejected;
+    }
+    for (size_t i = 0; i < bytes.size(); ++i) {  // one flipped byte
+        std::vector<unsigned char> b = bytes;
+        b[i] ^= 0x5a;
+        write(b);
+        const int rc = rtiLoadAccum(bad.c_str(), back.data(), &w, &h, &f);
+        if (rc == RT_SUCCESS) std::abort();
+        ++g_rejected;
+    }
+    w = W + 1;  // a caller expecting another size
+    std::vector<float> small(4 * 2 * 2);
+    if (rtiLoadAccum(path.c_str(), small.data(), &w, &h, &f) == RT_SUCCESS && (w != W || h != H)) std::abort();
+    if (rtiLoadAccum((g_dir + "/missing.bin").c_str(), nullptr, &w, &h, &f) == RT_SUCCESS) std::abort();
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: sanitize_main SCRATCH_DIR\n");
@@ -225,6 +266,7 @@ int main(int argc, char** argv) {
     const std::string empty_mtl;
     try_obj("emptymtl", grid_mesh(2, false), &empty_mtl);
     soups();
+    checkpoints();
     std::printf("sanitize: %d scenes built, %d inputs rejected, no sanitizer reports\n", g_scenes, g_rejected);
     return 0;
 }
