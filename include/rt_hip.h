@@ -363,6 +363,13 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
  * may share one device (several ranks on one GPU), so the N > 1 gather runs where there is only
  * one GPU.  Every gather and reduction must pass all n communicators (n_local == n); n <= 64. */
 int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out);
+/* A world of processes on one node WITHOUT RCCL -- e.g. several ranks sharing one GPU, which RCCL
+ * refuses: rank `rank` of `nranks`, one process each, meeting through files in the directory `dir`
+ * (the same for every rank, empty, on a file system they share; the caller removes it after
+ * rtCommDestroy).  Setup exchanges, rtCommAllReduceF64 and rtCommBarrier go through the files
+ * (each waits at most a minute for the slowest rank); the gathers run on the copy engines over
+ * IPC mappings exactly as in an RCCL world (RT_COMM_TRANSPORT_RCCL is refused). */
+int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_comm* out);
 int rtCommDestroy(rt_comm comm);
 int rtCommGetRank(rt_comm comm, int* rank, int* nranks);
 /* The kernel renders this rank's bands: rtKernelSetRowInterleave(k, nranks, rank).  The gather's

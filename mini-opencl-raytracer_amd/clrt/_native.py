@@ -148,6 +148,7 @@ _HIP_PROTOS = {
     "rtCommInitRank": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.POINTER(_vp)]),
     "rtCommInitAll": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(_vp)]),
     "rtCommInitLoopback": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rtCommInitShared": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "rtCommDestroy": (ctypes.c_int, [_vp]),
     "rtCommGetRank": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "rtCommShardKernel": (ctypes.c_int, [_vp, _vp]),

@@ -169,6 +169,16 @@ class Comm:
         check(N.hip_lib().rtCommInitLoopback(hs, n, out), "comm init loopback")
         return [cls(out[i], ctxs[i]) for i in range(n)]
 
+    @classmethod
+    def init_shared(cls, ctx, nranks: int, rank: int, directory: str) -> "Comm":
+        """A world of processes on one node without RCCL (rtCommInitShared): setup and reductions
+        through files in `directory`, gathers on the copy engines over IPC mappings -- several
+        ranks may share one GPU."""
+        h = ctypes.c_void_p()
+        check(N.hip_lib().rtCommInitShared(ctx.handle, nranks, rank, directory.encode(), ctypes.byref(h)),
+              "comm init shared")
+        return cls(h.value, ctx)
+
     def set_transport(self, transport: int) -> None:
         """rtCommSetTransport: N.COMM_TRANSPORT_COPY_ENGINES (default) or N.COMM_TRANSPORT_RCCL."""
         check(self._lib.rtCommSetTransport(self.handle, transport), "comm transport")

@@ -33,7 +33,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <thread>
 #include <new>
 #include <vector>
@@ -129,6 +131,10 @@ struct rt_comm_s {
     // (0.790 vs 0.798 ms/frame) and 8 stalled the renders (1.17; profiles/r04/dist_flow_ab.txt)
     hipStream_t xstream[8] = {};
     hipEvent_t xgo = nullptr, xdone[8] = {};
+    // shared worlds (rtCommInitShared): no RCCL; setup exchanges, reductions and barriers go
+    // through files in `fdir` (exchange number fseq), the gathers over the copy engines
+    std::string fdir;
+    uint64_t fseq = 0;
 };
 
 namespace {
@@ -325,6 +331,57 @@ int link_direct(const rt_comm* comms, int n_local, int root) {
 // root: receive slots and arrival flags; everyone: slot-free flags) with one ncclAllGather, maps
 // the ones it needs, and the world agrees (ncclAllReduce, max) whether every rank could -- if
 // one could not, the whole world keeps the RCCL transport for this plan.
+// Shared worlds: an all-gather of `n` bytes per rank through files -- each rank writes
+// x<seq>_r<rank> (written to a temporary name, then renamed, so a reader never sees half a file)
+// and reads everyone's, waiting up to a minute for the slowest rank.
+int file_allgather(rt_comm c, const void* mine, size_t n, void* all) {
+    const uint64_t seq = ++c->fseq;
+    auto name = [&](int q) { return c->fdir + "/x" + std::to_string(seq) + "_r" + std::to_string(q); };
+    {
+        const std::string tmp = name(c->rank) + ".tmp";
+        std::FILE* f = std::fopen(tmp.c_str(), "wb");
+        if (!f) return RT_FILE_NOT_FOUND;
+        const bool ok = std::fwrite(mine, 1, n, f) == n;
+        if (std::fclose(f) != 0 || !ok || std::rename(tmp.c_str(), name(c->rank).c_str()) != 0) return RT_OUT_OF_RESOURCES;
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+    for (int q = 0; q < c->nranks; ++q) {
+        for (;;) {
+            std::FILE* f = std::fopen(name(q).c_str(), "rb");
+            if (f) {
+                const bool ok = std::fread(static_cast<uint8_t*>(all) + (size_t)q * n, 1, n, f) == n;
+                std::fclose(f);
+                if (!ok) return RT_PARSE_ERROR;
+                break;
+            }
+            if (std::chrono::steady_clock::now() > deadline) return RT_OUT_OF_RESOURCES;
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+    }
+    return RT_SUCCESS;
+}
+
+// the world's maximum of v (RCCL, or files in a shared world)
+int world_max(rt_comm c, int v, int* out) {
+    if (!c->fdir.empty()) {
+        std::vector<int> all(c->nranks);
+        int rc = file_allgather(c, &v, sizeof(v), all.data());
+        if (rc) return rc;
+        *out = *std::max_element(all.begin(), all.end());
+        return RT_SUCCESS;
+    }
+    int* d = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d), 2 * sizeof(int));
+    if (e != hipSuccess) return map_hip(e);
+    e = hipMemcpy(d, &v, sizeof(int), hipMemcpyHostToDevice);
+    int rc = map_hip(e);
+    if (!rc) rc = map_nccl(ncclAllReduce(d, d + 1, 1, ncclInt32, ncclMax, c->nc, c->cstream));
+    if (!rc) rc = map_hip(hipStreamSynchronize(c->cstream));
+    if (!rc) rc = map_hip(hipMemcpy(out, d + 1, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return rc;
+}
+
 struct IpcBlob {
     hipIpcMemHandle_t parts[2], rflags, sflags;
 };
@@ -405,20 +462,20 @@ int link_ipc(rt_comm c) {
     }
     if (e != hipSuccess) bad = 1;
     std::vector<IpcBlob> all(c->nranks);
-    void* dev = nullptr;
-    const size_t nb = sizeof(IpcBlob) * (c->nranks + 1) + sizeof(int) * 2;
-    e = hipMalloc(&dev, nb);
-    if (e != hipSuccess) return map_hip(e);
-    uint8_t* d = static_cast<uint8_t*>(dev);
     auto exchange = [&]() -> int {
-        hipError_t he = hipMemcpy(d, &mine, sizeof(mine), hipMemcpyHostToDevice);
+        if (!c->fdir.empty()) return file_allgather(c, &mine, sizeof(mine), all.data());
+        void* dev = nullptr;
+        hipError_t he = hipMalloc(&dev, sizeof(IpcBlob) * (c->nranks + 1));
         if (he != hipSuccess) return map_hip(he);
-        int rc = map_nccl(ncclAllGather(d, d + sizeof(IpcBlob), sizeof(IpcBlob), ncclUint8, c->nc, c->cstream));
-        if (rc) return rc;
-        he = hipStreamSynchronize(c->cstream);
-        if (he == hipSuccess)
-            he = hipMemcpy(all.data(), d + sizeof(IpcBlob), sizeof(IpcBlob) * c->nranks, hipMemcpyDeviceToHost);
-        return map_hip(he);
+        uint8_t* d = static_cast<uint8_t*>(dev);
+        he = hipMemcpy(d, &mine, sizeof(mine), hipMemcpyHostToDevice);
+        int rc = map_hip(he);
+        if (!rc) rc = map_nccl(ncclAllGather(d, d + sizeof(IpcBlob), sizeof(IpcBlob), ncclUint8, c->nc, c->cstream));
+        if (!rc) rc = map_hip(hipStreamSynchronize(c->cstream));
+        if (!rc)
+            rc = map_hip(hipMemcpy(all.data(), d + sizeof(IpcBlob), sizeof(IpcBlob) * c->nranks, hipMemcpyDeviceToHost));
+        (void)hipFree(dev);
+        return rc;
     };
     auto open = [&](const hipIpcMemHandle_t& h, void** p) {
         if (bad) return;
@@ -455,31 +512,17 @@ int link_ipc(rt_comm c) {
             c->peer_rflags = static_cast<uint64_t*>(p[2]);
         }
         // does every rank hold its links?
-        int* flag = reinterpret_cast<int*>(d + sizeof(IpcBlob) * (c->nranks + 1));
-        hipError_t he = hipMemcpy(flag, &bad, sizeof(int), hipMemcpyHostToDevice);
-        if (he == hipSuccess) {
-            rc = map_nccl(ncclAllReduce(flag, flag + 1, 1, ncclInt32, ncclMax, c->nc, c->cstream));
-            if (!rc) he = hipStreamSynchronize(c->cstream);
-            if (!rc && he == hipSuccess) he = hipMemcpy(&bad, flag + 1, sizeof(int), hipMemcpyDeviceToHost);
-        }
-        if (!rc && he != hipSuccess) rc = map_hip(he);
+        rc = world_max(c, bad, &bad);
     }
     // the links hold: one small transfer and both flags across the world, polled from the host
     // with a deadline, before any gather relies on them (a world whose first real gather waited on
     // a flag that never arrives would hang instead of falling back)
     if (!rc && !bad) {
         bad = ipc_handshake(c);
-        int* flag = reinterpret_cast<int*>(d + sizeof(IpcBlob) * (c->nranks + 1));
-        hipError_t he = hipMemcpy(flag, &bad, sizeof(int), hipMemcpyHostToDevice);
-        if (he == hipSuccess) {
-            rc = map_nccl(ncclAllReduce(flag, flag + 1, 1, ncclInt32, ncclMax, c->nc, c->cstream));
-            if (!rc) he = hipStreamSynchronize(c->cstream);
-            if (!rc && he == hipSuccess) he = hipMemcpy(&bad, flag + 1, sizeof(int), hipMemcpyDeviceToHost);
-        }
-        if (!rc && he != hipSuccess) rc = map_hip(he);
+        rc = world_max(c, bad, &bad);
     }
-    (void)hipFree(dev);
     if (rc) return rc;
+    if (bad && !c->nc) return RT_INVALID_OPERATION;  // a shared world has no RCCL to fall back to
     if (bad) {  // the world falls back to RCCL transfers for this plan
         for (void* p : c->ipc_opened) (void)hipIpcCloseMemHandle(p);
         c->ipc_opened.clear();
@@ -629,6 +672,33 @@ int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
     return RT_SUCCESS;
 }
 
+int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_comm* out) {
+    if (!out) return RT_INVALID_VALUE;
+    *out = nullptr;
+    if (!ctx) return RT_INVALID_CONTEXT;
+    if (!dir || !*dir || nranks < 1 || rank < 0 || rank >= nranks) return RT_INVALID_VALUE;
+    hipError_t he = hipSetDevice(ctx->device);
+    if (he != hipSuccess) return map_hip(he);
+    rt_comm c = new (std::nothrow) rt_comm_s();
+    if (!c) return RT_OUT_OF_HOST_MEMORY;
+    c->ctx = ctx;
+    c->rank = rank;
+    c->nranks = nranks;
+    try {
+        c->fdir = dir;
+    } catch (const std::bad_alloc&) {
+        delete c;
+        return RT_OUT_OF_HOST_MEMORY;
+    }
+    const int rc = comm_streams(c, false);
+    if (rc) {
+        release(c);
+        return rc;
+    }
+    *out = c;
+    return RT_SUCCESS;
+}
+
 int rtCommDestroy(rt_comm c) {
     if (!c) return RT_INVALID_VALUE;
     (void)hipSetDevice(c->ctx->device);
@@ -650,6 +720,7 @@ int rtCommSetTransport(rt_comm c, int transport) {
         transport != RT_COMM_TRANSPORT_COPY_ENGINES_IPC)
         return RT_INVALID_VALUE;
     if (c->group && transport != RT_COMM_TRANSPORT_COPY_ENGINES) return RT_INVALID_OPERATION;
+    if (!c->nc && transport == RT_COMM_TRANSPORT_RCCL) return RT_INVALID_OPERATION;  // shared worlds
     if (transport == c->transport) return RT_SUCCESS;
     (void)hipSetDevice(c->ctx->device);
     (void)hipStreamSynchronize(c->cstream);
@@ -702,7 +773,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     if (fresh && comms[0]->transport != RT_COMM_TRANSPORT_RCCL) {
         int rc = RT_SUCCESS;
         if (comms[0]->transport == RT_COMM_TRANSPORT_COPY_ENGINES_IPC) {
-            if (n_local != 1 || !comms[0]->nc) return RT_INVALID_OPERATION;
+            if (n_local != 1 || (!comms[0]->nc && comms[0]->fdir.empty())) return RT_INVALID_OPERATION;
             rc = link_ipc(comms[0]);
         } else if (n_local == comms[0]->nranks) {
             rc = link_direct(comms, n_local, root);  // every member is in this call
@@ -710,14 +781,15 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
                 for (int i = 0; i < n_local; ++i) comms[i]->ce = false;
                 rc = RT_SUCCESS;
             }
-        } else if (n_local == 1 && comms[0]->nc) {
+        } else if (n_local == 1 && (comms[0]->nc || !comms[0]->fdir.empty())) {
             rc = link_ipc(comms[0]);
         }
         if (rc) return rc;
     }
     bool ce = true;
     for (int i = 0; i < n_local; ++i) ce &= comms[i]->ce;
-    if (comms[0]->group && !ce) return RT_INVALID_OPERATION;  // a loopback world moves bytes on copy engines
+    // loopback and shared worlds move bytes on the copy engines only
+    if ((comms[0]->group || !comms[0]->fdir.empty()) && !ce) return RT_INVALID_OPERATION;
     if (ce) return ce_gather(comms, n_local, root, root_dst, outs);
     // RCCL transport.  Phase 1: every rank (the root too) packs its bands on its context's
     // accumulation stream
@@ -947,6 +1019,28 @@ int rtCommAllReduceF64(const rt_comm* comms, int n_local, double* values, int co
     for (int i = 0; i < n_local; ++i)
         if (!comms[i]) return RT_INVALID_VALUE;
     if (int rc = check_loopback(comms, n_local)) return rc;
+    if (!comms[0]->fdir.empty()) {
+        // shared world: one rank per call, the reduction through the exchange files, after this
+        // rank's earlier gathers have drained (as RCCL's stream order would have it)
+        if (n_local != 1) return RT_INVALID_VALUE;
+        rt_comm c = comms[0];
+        hipError_t e = hipSetDevice(c->ctx->device);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->cstream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->ustream);
+        if (e != hipSuccess) return map_hip(e);
+        std::vector<double> all((size_t)c->nranks * count);
+        int rc = file_allgather(c, values, sizeof(double) * count, all.data());
+        if (rc) return rc;
+        for (int j = 0; j < count; ++j) {
+            double acc = all[j];
+            for (int q = 1; q < c->nranks; ++q) {
+                const double v = all[(size_t)q * count + j];
+                acc = op == RT_COMM_SUM ? acc + v : std::max(acc, v);
+            }
+            values[j] = acc;
+        }
+        return RT_SUCCESS;
+    }
     if (comms[0]->group) {
         // loopback world: every member is here, so the reduction is over these rows, after the
         // members' communicator streams (earlier gathers) have drained, as RCCL's would
