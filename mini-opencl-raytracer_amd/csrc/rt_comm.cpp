@@ -247,6 +247,11 @@ void release(rt_comm c) {
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
     // the last communicator of the context gives its CUs back to the renders
     if (c->reserved && --c->ctx->reserve_refs == 0) (void)rti::reserve_cus(c->ctx, 0, nullptr);
+    // a shared world's rank removes its own exchange files but the last: every rank wrote its file
+    // of exchange k only after reading all files of exchange k - 1, so those have all been read;
+    // the last one may still be awaited by a slower rank (the caller removes the directory)
+    for (uint64_t q = 1; !c->fdir.empty() && q < c->fseq; ++q)
+        (void)std::remove((c->fdir + "/x" + std::to_string(q) + "_r" + std::to_string(c->rank)).c_str());
     delete c;
 }
 
