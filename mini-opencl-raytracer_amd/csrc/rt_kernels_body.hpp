@@ -15,8 +15,8 @@
 //     ray's octant, so it is replayed exactly with per-octant skip pointers (8 per
 //     node, built on the host): node visits, triangle tests and their order are the
 //     reference's, without LDS pushes/pops or the dependent pop latency;
-//   * traversal keeps only {t, primitive}; the hit record (position, shading normal,
-//     material) is formed once after the walk from the last accepted triangle, which
+//   * traversal keeps {t, primitive, u, v} (RT_KEEP_UV); the hit record (position, shading
+//     normal, material) is formed once after the walk from the last accepted triangle, which
 //     yields the same values as the reference forming it at every accept;
 //   * no MFMA: this is branchy, latency-bound traversal.
 // Parity: every arithmetic step follows the reference's operation order with
