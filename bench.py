@@ -40,6 +40,8 @@ import hashlib
 import json
 import os
 import sys
+import shutil
+import tempfile
 import time
 
 import numpy as np
@@ -100,6 +102,10 @@ def parse():
                    help="N>1: how the gather moves the bands (rtCommSetTransport): copy engines over xGMI "
                         "(default), RCCL send/recv kernels, or copy engines linked by IPC handles even at "
                         "world size 1 (the multi-process path)")
+    p.add_argument("--shared-world", action="store_true",
+                   help="N>1 with every rank on GPU 0 and no RCCL (rtCommInitShared: setup through files, "
+                        "gathers over IPC mappings on the copy engines) -- the N>1 orchestration on a one-GPU box; "
+                        "not a scaling measurement (the ranks share one GPU)")
     p.add_argument("--check-gather", action="store_true",
                    help="after timing, rank 0 renders the whole frame unsharded and checks the gathered "
                         "image against it byte for byte")
@@ -330,11 +336,21 @@ def main():
                                             method="lbvh" if args.bvh == "device-lbvh" else "ploc")
 
     comm = None
+    shared_dir = None
     if world > 1 or args.force_dist:
         # one rank per GPU: rank 0's RCCL id reaches the others through a file on this node
-        ctx = clrt.CLContext(local)
-        uid = mg.file_rendezvous(rank, world, mg.Comm.unique_id)
-        comm = mg.Comm.init_rank(ctx, world, uid, rank)
+        if args.shared_world:
+            # every rank on GPU 0; rank 0 makes the world's exchange directory and hands its name to
+            # the others through the same per-launch file as the RCCL id
+            ctx = clrt.CLContext(0)
+            tok = mg.file_rendezvous(rank, world, lambda: tempfile.mkdtemp(prefix="rt_shared_").encode().ljust(
+                N.COMM_ID_BYTES, b"\0"))
+            shared_dir = tok.rstrip(b"\0").decode()
+            comm = mg.Comm.init_shared(ctx, world, rank, shared_dir)
+        else:
+            ctx = clrt.CLContext(local)
+            uid = mg.file_rendezvous(rank, world, mg.Comm.unique_id)
+            comm = mg.Comm.init_rank(ctx, world, uid, rank)
         mg.Comm.barrier([comm])
         if rank == 0:
             mg.rendezvous_cleanup()
@@ -416,7 +432,15 @@ def main():
         rl["accum_ms_per_launch"] = round(ks["accum_ms"] / launches, 4)
     if rank != 0:
         comm.destroy()
+        if shared_dir:  # tell rank 0 this rank is done with the exchange files
+            open(os.path.join(shared_dir, f"done_{rank}"), "w").close()
         return
+    if shared_dir:  # the directory goes once every other rank has left it
+        t0 = time.monotonic()
+        while (time.monotonic() - t0 < 30 and
+               not all(os.path.exists(os.path.join(shared_dir, f"done_{q}")) for q in range(1, world))):
+            time.sleep(0.01)
+        shutil.rmtree(shared_dir, ignore_errors=True)
     scene_name = "Cornell box" if args.scene == "cornell" else "bunny-class proxy, 69,692 triangles"
     line = {
         "metric": f"Mrays/s ({args.width}x{args.height} {scene_name}, {args.frames} spp, {args.bounces} bounces)",
@@ -437,6 +461,7 @@ def main():
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
                    "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh,
                    "parallelism": f"interleaved 8-row bands x{world}" + (
+                       (" (shared world: every rank on GPU 0, no RCCL)" if args.shared_world else "") +
                        f" + gather to rank 0 over {'RCCL' if args.transport == 'rccl' else 'copy engines'}"
                        " (librt_hip rtCommEnqueueGatherBands"
                        + (", host-synchronised)" if args.gather_sync else ", pipelined with the next step)")
