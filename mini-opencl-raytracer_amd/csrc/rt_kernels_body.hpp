@@ -1560,6 +1560,24 @@ __device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32
     return v;
 }
 
+// Flagless radiance sets (flagTiles 2) store a primary miss as (K_rad, K_rad, K_rad) like any other
+// radiance: the sky shortcut's frame flags are read back from the frames themselves, all set only
+// when every frame holds K_rad (a pixel whose old value is not K_old never asks; the first frame
+// that is not K_rad ends the scan).  The chain would read the same bits, so the flags change which
+// path writes K_out, never a value.  A/B: -DRT_NOFLAG_SKYSCAN=0.
+#ifndef RT_NOFLAG_SKYSCAN
+#define RT_NOFLAG_SKYSCAN 1
+#endif
+__device__ __forceinline__ uint32_t scan_sky_frames(const KernelArgs& a, uint32_t gid, float krad) {
+    const uint32_t k = __float_as_uint(krad);
+#pragma unroll 1
+    for (uint32_t s = 0; s < a.nFrames; ++s) {
+        const float4 r = rad_load(a.radBuf + (size_t)s * a.radStride + gid);
+        if (__float_as_uint(r.x) != k || __float_as_uint(r.y) != k || __float_as_uint(r.z) != k) return 0u;
+    }
+    return (1u << a.nFrames) - 1u;
+}
+
 template <class M>
 __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* key) {
     if (threadIdx.x != 0) return;
@@ -1630,10 +1648,12 @@ __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uin
         float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (live) {
             if (a.frameCount != 0u) o = a.result[gid];
-            fl = a.flagTiles == 1u ? load_tile_flags(a, tile, lane) : a.flagTiles == 2u ? 0u : load_flags(a, gid);
-            sky = fl == (1u << a.nFrames) - 1u &&
-                  (a.frameCount == 0u ||
-                   (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold));
+            const bool old_sky = a.frameCount == 0u ||
+                                 (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold);
+            fl = a.flagTiles == 1u ? load_tile_flags(a, tile, lane)
+                 : a.flagTiles == 2u ? (RT_NOFLAG_SKYSCAN && old_sky ? scan_sky_frames(a, gid, krf) : 0u)
+                                     : load_flags(a, gid);
+            sky = fl == (1u << a.nFrames) - 1u && old_sky;
             if (sky) {
                 const float v = __uint_as_float(kout);
                 a.result[gid] = make_float4(v, v, v, 0.0f);
