@@ -89,17 +89,22 @@ def test_fused_other_schedules_launch_per_frame(cornell):
     _same(_render(cornell, W, H, 1, 3, True, sched=N.SCHED_TILES), _render(cornell, W, H, 1, 3, False))
 
 
-def test_fused_sky_shortcut_chain(cornell):
+@pytest.mark.parametrize("force_global", [False, True])
+def test_fused_sky_shortcut_chain(cornell, force_global):
     """Repeated fused calls (the sky key chains from the previous call's result), a skybox change,
     a math-mode switch and a restart at frame 1 over a non-sky history: every call's output equals
-    the per-frame launches (16:9 view: about half of the pixels see only sky)."""
+    the per-frame launches (16:9 view: about half of the pixels see only sky).  force_global: the
+    octant walk over HBM/L2, whose radiance sets carry no flags -- the accumulation reads a pixel's
+    all-sky frames back from the radiance itself (RT_NOFLAG_SKYSCAN)."""
     W, H = 320, 180
     seq = [(1, 4, 1.0, N.MATH_SHIPPED), (5, 4, 1.0, N.MATH_SHIPPED), (1, 8, 1.0, N.MATH_SHIPPED),
            (1, 3, 0.6, N.MATH_SHIPPED), (4, 2, 0.6, N.MATH_DEVICELIB), (0, 2, 2.0, N.MATH_PINNED),
            (1, 2, 2.0, N.MATH_PINNED)]
     outs = []
     for fused in (True, False):
-        r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, hits=True)
+        r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, hits=True, force_global=force_global)
+        if force_global:
+            r.k.set_tuning("global_oct", 1)
         got = []
         for first, n, sky, math in seq:
             r.k.set_math_mode(math)
