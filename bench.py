@@ -109,6 +109,9 @@ def parse():
     p.add_argument("--check-gather", action="store_true",
                    help="after timing, rank 0 renders the whole frame unsharded and checks the gathered "
                         "image against it byte for byte")
+    p.add_argument("--fail-links", action="store_true",
+                   help="test hook (rtCommSetOption RT_COMM_OPT_FAIL_LINKS): this rank reports its copy-engine "
+                        "links as broken, so the world takes the RCCL fallback -- which the line then reports")
     return p.parse_args()
 
 
@@ -314,6 +317,34 @@ def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts,
     return rl
 
 
+def comm_report(comm, ks, args):
+    """What the N > 1 flow actually ran, rank by rank, gathered to every rank (collective): the
+    communicator's world size, each rank's effective transport (a world whose copy-engine links
+    fail falls back to RCCL -- reported here, never hidden), its render launch time and its last
+    gather's transfer time."""
+    fields = 7
+    launches = max(1, ks["launches"])
+    st = comm.status()
+    mine = [float(st["active_code"]), float(st["fallback"]),
+            float([k for k, v in N.COMM_FALLBACK_NAMES.items() if v == st["fallback_reason"]][0]),
+            ks["render_period_ms"] if ks["render_period_ms"] > 0 else ks["kernel_ms"] / launches,
+            -1.0 if st["last_xfer_ms"] is None else st["last_xfer_ms"],
+            float(st["bytes_per_gather"]), float(st["copies_per_gather"])]
+    vec = np.zeros(comm.nranks * fields)
+    vec[comm.rank * fields:(comm.rank + 1) * fields] = mine
+    for i in range(0, len(vec), 64):  # (rtCommAllReduceF64 takes up to 64 values per call)
+        vec[i:i + 64] = mg.Comm.allreduce([comm], [vec[i:i + 64]], N.COMM_SUM)[0]
+    per = vec.reshape(comm.nranks, fields)
+    ranks = [{"rank": q, "transport": N.COMM_TRANSPORT_NAMES[int(p[0])],
+              "fallback": N.COMM_FALLBACK_NAMES[int(p[2])] if p[1] else None,
+              "render_ms": round(p[3], 4), "last_gather_ms": None if p[4] < 0 else round(p[4], 4),
+              "bytes_per_gather": int(p[5]), "copies_per_gather": int(p[6])} for q, p in enumerate(per)]
+    kinds = sorted({r["transport"] for r in ranks})
+    return {"nranks": comm.nranks, "requested": N.COMM_TRANSPORT_NAMES[comm.transport()[0]],
+            "effective": kinds[0] if len(kinds) == 1 else "mixed: " + ", ".join(kinds),
+            "fallback": any(r["fallback"] for r in ranks), "per_rank": ranks}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,6 +393,8 @@ def main():
     if comm is not None:
         comm.set_transport({"rccl": N.COMM_TRANSPORT_RCCL, "copy": N.COMM_TRANSPORT_COPY_ENGINES,
                             "copy-ipc": N.COMM_TRANSPORT_COPY_ENGINES_IPC}[args.transport])
+        if args.fail_links:
+            comm.set_option(N.COMM_OPT_FAIL_LINKS, 1)
         if rank == 0:
             img = r.ctx.create_buffer(N.MEM_READ_WRITE, r.W * r.H * 16)
 
@@ -396,8 +429,10 @@ def main():
     elapsed = time.perf_counter() - t0
     ks = r.k.stats()
     r.k.set_timing(False)
+    comm_line = None
     if comm is not None:
         elapsed = float(mg.Comm.allreduce([comm], [elapsed], N.COMM_MAX)[0][0])
+        comm_line = comm_report(comm, ks, args)
 
     check = None
     if args.check_gather and comm is not None and rank == 0:
@@ -446,7 +481,7 @@ def main():
         "metric": f"Mrays/s ({args.width}x{args.height} {scene_name}, {args.frames} spp, {args.bounces} bounces)",
         "value": round(value, 3),
         "unit": "Mrays/s",
-        "n_gpus": world,
+        "n_gpus": comm.nranks if comm is not None else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
@@ -460,9 +495,9 @@ def main():
         "config": {"workload": f"{args.scene} {args.width}x{args.height} {args.frames}spp {args.bounces}-bounce path trace",
                    "width": args.width, "height": args.height, "frames": args.frames, "bounces": args.bounces,
                    "math": args.math, "schedule": args.sched, "launch": args.launch, "bvh": args.bvh,
-                   "parallelism": f"interleaved 8-row bands x{world}" + (
+                   "parallelism": f"interleaved 8-row bands x{comm.nranks if comm is not None else world}" + (
                        (" (shared world: every rank on GPU 0, no RCCL)" if args.shared_world else "") +
-                       f" + gather to rank 0 over {'RCCL' if args.transport == 'rccl' else 'copy engines'}"
+                       f" + gather to rank 0 over {comm_line['effective']}"
                        " (librt_hip rtCommEnqueueGatherBands"
                        + (", host-synchronised)" if args.gather_sync else ", pipelined with the next step)")
                        if comm is not None else ""),
@@ -470,6 +505,8 @@ def main():
                    "tuning": args.tune or None},
         "roofline": rl,
     }
+    if comm_line is not None:
+        line["comm"] = comm_line
     if check:
         line["check_gather"] = check
     if world == 1 and comm is None and args.launch == "fused" and not args.no_drop_in:

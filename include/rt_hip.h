@@ -286,10 +286,12 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     work items when the host has not waited on the context
  *                                     through this API (rtFinish, a blocking read or write) since
  *                                     the kernel's previous per-frame launch -- i.e. frames are
- *                                     being queued.  A host that synchronises some other way
- *                                     (hipStreamSynchronize on rtContextGetStream's stream,
- *                                     hipDeviceSynchronize, events) looks like a queueing host to
- *                                     this rule and should set 0.  Results never change.
+ *                                     being queued -- and no stream or device pointer of the
+ *                                     context has been handed out (rtContextGetStream,
+ *                                     rtContextGetAccumStream, rtBufferGetDevicePointer: the host
+ *                                     may then synchronise outside the library, which this rule
+ *                                     cannot see; such a host's frames launch on the main stream,
+ *                                     at once -- see PERFRAME_BATCH).  Results never change.
  *   PERFRAME_DEFER_MIN                work items from which PERFRAME_DEFER 2 defers (default 4 Mi)
  *   MAX_BLOCKS                        persistent schedules: workgroups per CU of the grid (0 =
  *                                     as many as fit, default; fewer = fewer waves per SIMD)
@@ -303,7 +305,13 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     -- so results are the same bits at every point the host can
  *                                     observe; kernels with stats or timing on are not coalesced.
  *                                     An error of a coalesced launch is returned by the next call
- *                                     on the context that returns one (rtFinish at the latest).
+ *                                     on the context that returns one (rtFinish at the latest; a
+ *                                     frame enqueued over such an error is not queued).  Once the
+ *                                     context's stream (rtContextGetStream, rtContextGetAccumStream)
+ *                                     or a device pointer of one of its buffers
+ *                                     (rtBufferGetDevicePointer) has been handed out, the host may
+ *                                     synchronise outside the library, so from then on every
+ *                                     rtEnqueueKernel launches at once.
  *   SPEC_WALK                         step schedule, LDS octant walk, builds with the speculative
  *                                     walk compiled in (RT_SPEC=1; the shipped build has it out,
  *                                     measured slower): 1 (default) = speculative walk (a lane
@@ -357,18 +365,20 @@ typedef struct rt_comm_s* rt_comm;
 int rtCommGetUniqueId(void* id /* RT_COMM_ID_BYTES */);
 int rtCommInitRank(rt_context ctx, int nranks, const void* id, int rank, rt_comm* out);
 int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
-/* A world of n ranks inside this process WITHOUT RCCL: the same sharding, pack, two-slot
- * pipelining and unpack as above, with the transfer step (grouped ncclSend/ncclRecv) replaced by
- * device copies into the root's receive slots on the root's communicator stream.  The contexts
- * may share one device (several ranks on one GPU), so the N > 1 gather runs where there is only
- * one GPU.  Every gather and reduction must pass all n communicators (n_local == n); n <= 64. */
+/* A world of n ranks inside this process WITHOUT RCCL: the same sharding and copy-engine gather as
+ * above, the ranks linked by address.  The contexts may share one device (several ranks on one
+ * GPU), so the N > 1 gather runs where there is only one GPU.  Every gather and reduction must
+ * pass all n communicators (n_local == n); n <= 64. */
 int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out);
 /* A world of processes on one node WITHOUT RCCL -- e.g. several ranks sharing one GPU, which RCCL
  * refuses: rank `rank` of `nranks`, one process each, meeting through files in the directory `dir`
- * (the same for every rank, empty, on a file system they share; the caller removes it after
- * rtCommDestroy).  Setup exchanges, rtCommAllReduceF64 and rtCommBarrier go through the files
- * (each waits at most a minute for the slowest rank); the gathers run on the copy engines over
- * IPC mappings exactly as in an RCCL world (RT_COMM_TRANSPORT_RCCL is refused). */
+ * (the same for every rank, empty, on a file system they share -- a directory that already holds
+ * exchange files is refused, RT_INVALID_VALUE; the caller removes it after rtCommDestroy).  Setup
+ * exchanges, rtCommAllReduceF64 and rtCommBarrier go through the files (each waits at most a
+ * minute for the slowest rank); the gathers run on the copy engines over IPC mappings exactly as
+ * in an RCCL world (RT_COMM_TRANSPORT_RCCL is refused).  It ships because it is the only way to
+ * run the one-process-per-GPU gather (IPC handles, the trial round, flags written into another
+ * process's memory) on a machine with one GPU: bench.py --shared-world and the GPU tests use it. */
 int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_comm* out);
 int rtCommDestroy(rt_comm comm);
 int rtCommGetRank(rt_comm comm, int* rank, int* nranks);
@@ -380,27 +390,40 @@ int rtCommShardKernel(rt_comm comm, rt_kernel k);
  * of 16 bytes, rendered after rtCommShardKernel) are assembled in the root's `root_dst` (NULL =
  * the root's own `out`).  `comms`/`outs`: the n_local communicators this host thread drives
  * (1 per process in the one-process-per-GPU setup) and their output buffers.  Asynchronous and
- * pipelined: each rank packs its bands after the fused-frame accumulations enqueued so far (on
- * the context's accumulation stream), the transport (rtCommSetTransport) moves them to the root
- * on the communicator's stream, and the root unpacks them on a third stream (gathering into its
- * own `out`, the root's own bands are in place: it neither sends nor unpacks them), so neither
- * the next fused render nor the next accumulation is held up by the transfer; two staging
- * slots, so step k's gather overlaps step k+1's render.  The communicator's streams run at the
- * device's greatest stream priority.  Every later call on a context that reads or writes memory
- * (rtFinish, rtEnqueueReadBuffer, per-frame launches, ...) is ordered after the gather. */
+ * pipelined, so neither the next fused render nor the next accumulation waits for a transfer:
+ *   copy engines (default transport): each rank's copy engine writes its bands, straight from
+ *     its `out` (after the fused-frame accumulations and per-frame launches enqueued so far),
+ *     into the rows they occupy in the root's destination -- no staging, no pack or unpack
+ *     kernel, no compute unit anywhere in the gather -- and raises an arrival flag in the root's
+ *     memory; the root's reads of the image wait for every flag.  The root's own bands are in
+ *     place when it gathers into its own `out`; else its copy engine copies them like any rank's.
+ *     A rank's copies of gather k start once the root has enqueued gather k and finished the
+ *     calls it queued before (reads of image k - 1): the root's image never changes under a read
+ *     queued on it.  The destination is part of the plan, with the size and the root: in a world
+ *     of one rank per process the root refuses (RT_INVALID_OPERATION) a gather into another
+ *     buffer until the plan is rebuilt (a size or root change, or rtCommSetTransport -- collective
+ *     steps); a destination released meanwhile stays allocated until then.
+ *   RCCL: each rank packs its bands into a staging slot on its accumulation stream, grouped
+ *     ncclSend/ncclRecv move the slots to the root on the communicator's stream, and the root
+ *     unpacks them on a third stream; two staging slots, so step k's gather overlaps step k+1's
+ *     render.
+ * The communicator's streams run at the device's greatest stream priority.  Every later call on a
+ * context that reads or writes memory (rtFinish, rtEnqueueReadBuffer, per-frame launches, ...) is
+ * ordered after its part of the gather. */
 int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_local, unsigned width,
                              unsigned height, int root, rt_mem root_dst);
-/* How the gather moves the packed bands (set alike on every rank, before a gather; a change
- * takes effect at the next gather, which rebuilds the plan -- a collective step):
- *   RT_COMM_TRANSPORT_COPY_ENGINES (default): each rank's copy engine (SDMA; over xGMI between
- *     GPUs) copies its staging slot into the root's receive slot -- mapped by IPC handle
- *     (exchanged with one ncclAllGather per plan) or, for ranks driven by one process, by address
- *     -- and signals arrival with a flag in the root's memory (hipStreamWriteValue64); the root's
- *     unpack waits on the flags (hipStreamWaitValue64) and raises per-rank slot-free flags.  No
+/* How the gather moves the bands (set alike on every rank, before a gather; a change takes effect
+ * at the next gather, which rebuilds the plan -- a collective step):
+ *   RT_COMM_TRANSPORT_COPY_ENGINES (default): the copy engines (SDMA; over xGMI between GPUs) write
+ *     every band into the root's destination -- mapped by IPC handle (exchanged with one
+ *     ncclAllGather per plan, then checked with one trial copy and flag round across the world)
+ *     or, for ranks driven by one process, by address.  Arrival and release are flags
+ *     (hipStreamWriteValue64 / hipStreamWaitValue64) between the processes, events within one.  No
  *     compute unit is used for the transfer, so it runs beside a persistent render.  A world in
- *     which some rank cannot map the root's memory falls back to RCCL transfers.
+ *     which some rank cannot map the root's memory falls back to RCCL transfers for the plan
+ *     (rtCommGetStatus reports it).
  *   RT_COMM_TRANSPORT_RCCL: grouped ncclSend/ncclRecv on the communicator stream (the root's own
- *     bands too: a device-local send), i.e. RCCL's transfer kernel.
+ *     bands too: a device-local send), i.e. RCCL's transfer kernel, with the pack and unpack copies.
  *   RT_COMM_TRANSPORT_COPY_ENGINES_IPC: the copy engines with the links always set up the
  *     multi-process way (IPC handles through ncclAllGather, a world-wide ncclAllReduce on the
  *     outcome) even when every rank is driven by this process -- the one-process-per-GPU path,
@@ -410,7 +433,31 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
 #define RT_COMM_TRANSPORT_RCCL 1
 #define RT_COMM_TRANSPORT_COPY_ENGINES_IPC 2
 int rtCommSetTransport(rt_comm comm, int transport);
+/* *transport: the requested one; *active: the one the current plan runs (-1: no plan yet). */
 int rtCommGetTransport(rt_comm comm, int* transport, int* active);
+/* What the communicator's current plan does (self-description for benchmarks and logs). */
+#define RT_COMM_FALLBACK_NONE 0
+#define RT_COMM_FALLBACK_NO_PEER_ACCESS 1  /* one process, several GPUs: no peer access */
+#define RT_COMM_FALLBACK_IPC_MAP 2         /* some rank could not export or map an IPC handle */
+#define RT_COMM_FALLBACK_HANDSHAKE 3       /* the trial copy / flag round failed or timed out */
+typedef struct rt_comm_status {
+    int rank, nranks;
+    int transport;         /* requested (rtCommSetTransport) */
+    int active;            /* the current plan's transport, -1 before the first gather */
+    int fallback;          /* 1: the plan asked for the copy engines and runs RCCL instead */
+    int fallback_reason;   /* RT_COMM_FALLBACK_* */
+    unsigned copies_per_gather;        /* copy commands this rank issues per gather */
+    unsigned long long bytes_per_gather;  /* bytes this rank moves per gather */
+    unsigned long long gathers;        /* gathers enqueued with the current plan */
+    double last_xfer_ms;   /* the last completed gather's transfer on this rank (its copies, or
+                              its RCCL transfer; -1: none measured) */
+} rt_comm_status;
+int rtCommGetStatus(rt_comm comm, rt_comm_status* out);
+/* Test hooks.  RT_COMM_OPT_FAIL_LINKS (value 1): this rank reports its copy-engine links as
+ * broken at the next plan's link step, so the world takes the RCCL fallback (what a world whose
+ * IPC mappings or trial round fail does). */
+#define RT_COMM_OPT_FAIL_LINKS 1
+int rtCommSetOption(rt_comm comm, int option, int value);
 /* Blocking reductions of `count` doubles per local rank (values: n_local x count, in place),
  * op RT_COMM_SUM or RT_COMM_MAX; rtCommBarrier = a one-value reduction. */
 #define RT_COMM_SUM 0

@@ -100,6 +100,20 @@ class Rect(ctypes.Structure):
 COMM_ID_BYTES = 128
 COMM_SUM, COMM_MAX = 0, 1
 COMM_TRANSPORT_COPY_ENGINES, COMM_TRANSPORT_RCCL, COMM_TRANSPORT_COPY_ENGINES_IPC = 0, 1, 2
+COMM_TRANSPORT_NAMES = {-1: "none", COMM_TRANSPORT_COPY_ENGINES: "copy engines",
+                        COMM_TRANSPORT_RCCL: "RCCL", COMM_TRANSPORT_COPY_ENGINES_IPC: "copy engines (IPC links)"}
+# rt_comm_status.fallback_reason
+COMM_FALLBACK_NAMES = {0: None, 1: "no peer access", 2: "IPC handle export/map failed",
+                       3: "link trial round failed"}
+COMM_OPT_FAIL_LINKS = 1  # test hook (rtCommSetOption)
+
+
+class CommStatus(ctypes.Structure):
+    """rt_comm_status (rt_hip.h)."""
+    _fields_ = [("rank", ctypes.c_int), ("nranks", ctypes.c_int), ("transport", ctypes.c_int),
+                ("active", ctypes.c_int), ("fallback", ctypes.c_int), ("fallback_reason", ctypes.c_int),
+                ("copies_per_gather", ctypes.c_uint), ("bytes_per_gather", ctypes.c_ulonglong),
+                ("gathers", ctypes.c_ulonglong), ("last_xfer_ms", ctypes.c_double)]
 
 _vp = ctypes.c_void_p
 _HIP_PROTOS = {
@@ -154,6 +168,8 @@ _HIP_PROTOS = {
     "rtCommShardKernel": (ctypes.c_int, [_vp, _vp]),
     "rtCommSetTransport": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rtCommGetTransport": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "rtCommGetStatus": (ctypes.c_int, [_vp, ctypes.POINTER(CommStatus)]),
+    "rtCommSetOption": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "rtCommEnqueueGatherBands": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_uint,
                                                 ctypes.c_uint, ctypes.c_int, _vp]),
     "rtCommAllReduceF64": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.POINTER(ctypes.c_double),

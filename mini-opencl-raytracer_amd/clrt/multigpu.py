@@ -189,6 +189,22 @@ class Comm:
         check(self._lib.rtCommGetTransport(self.handle, ctypes.byref(t), ctypes.byref(a)), "comm transport")
         return t.value, a.value
 
+    def status(self) -> dict:
+        """rtCommGetStatus: what the current plan does -- the effective transport, whether the
+        copy-engine links fell back to RCCL (and why), the bytes and copy commands this rank
+        moves per gather, the last gather's transfer time on this rank."""
+        st = N.CommStatus()
+        check(self._lib.rtCommGetStatus(self.handle, ctypes.byref(st)), "comm status")
+        return {"rank": st.rank, "nranks": st.nranks, "transport": N.COMM_TRANSPORT_NAMES[st.transport],
+                "active": N.COMM_TRANSPORT_NAMES[st.active], "active_code": st.active,
+                "fallback": bool(st.fallback), "fallback_reason": N.COMM_FALLBACK_NAMES.get(st.fallback_reason),
+                "copies_per_gather": st.copies_per_gather, "bytes_per_gather": st.bytes_per_gather,
+                "gathers": st.gathers, "last_xfer_ms": None if st.last_xfer_ms < 0 else st.last_xfer_ms}
+
+    def set_option(self, option: int, value: int) -> None:
+        """rtCommSetOption (test hooks: N.COMM_OPT_FAIL_LINKS)."""
+        check(self._lib.rtCommSetOption(self.handle, option, value), "comm option")
+
     def shard(self, kernel) -> None:
         """The kernel renders this rank's interleaved bands (rtCommShardKernel)."""
         check(self._lib.rtCommShardKernel(self.handle, kernel.handle), "shard kernel")

@@ -712,10 +712,14 @@ int rtCreateBuffer(rt_context ctx, uint64_t flags, size_t size, const void* host
 }
 
 int rtReleaseBuffer(rt_mem m) {
-    if (!m) return RT_INVALID_MEM_OBJECT;
+    if (!m || m->released) return RT_INVALID_MEM_OBJECT;
     int rc = ensure_device(m->ctx);
     if (rc) return rc;
     (void)hipStreamSynchronize(qs(m->ctx));
+    if (m->pins > 0) {  // a gather plan still writes into it: freed when the plan lets go
+        m->released = true;
+        return RT_SUCCESS;
+    }
     (void)hipFree(m->dptr);
     delete m;
     return RT_SUCCESS;
@@ -807,6 +811,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
 }  // extern "C"
 
+void rti::unpin(rt_mem m) {
+    if (--m->pins > 0 || !m->released) return;
+    (void)hipFree(m->dptr);  // (the plan has synchronised the streams that wrote it)
+    delete m;
+}
+
 int rti::flush_frames(rt_context ctx) {
     if (!ctx || !ctx->pend_k) return RT_SUCCESS;
     rt_kernel k = ctx->pend_k;
@@ -838,8 +848,11 @@ extern "C" {
 // test_fused_frames.py), one launch tail per run instead of one per frame.  The frame is checked
 // here as a launch would check it, so argument and scene errors still come back from this call.
 int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
+    // (not once a stream or a device pointer of the context has been handed out: the host may then
+    // synchronise behind the library's back, e.g. hipStreamSynchronize on the exposed stream, and
+    // must find every frame it enqueued launched)
     const bool coalesce = ctx && k && k->ctx == ctx && k->pf_batch > 1 && k->sched == RT_SCHED_STEP && !k->stats &&
-                          !k->timing;
+                          !k->timing && !ctx->mexposed && !ctx->dexposed;
     if (!coalesce) {
         if (ctx && ctx->pend_k) {
             const int rc = rti::flush_frames(ctx);
@@ -860,10 +873,13 @@ int rtEnqueueKernel(rt_context ctx, rt_kernel k, size_t global_work_size) {
     if (k->bufs[RT_ARG_BUFFER_OUT]->size < global_work_size * 16) return RT_INVALID_GLOBAL_WORK_SIZE;
     if (k->hit_ids && (k->hit_ids->size < (global_work_size + kHitPad) * 4 || k->hit_t->size < global_work_size * 4))
         return RT_INVALID_MEM_OBJECT;
+    // an error of an earlier held launch is reported now, and this frame is not queued: the
+    // caller retrying it starts a fresh run instead of accumulating it twice
+    if (ctx->pend_error != RT_SUCCESS) return pending_error(ctx, RT_SUCCESS);
     if (ctx->pend_k == k && ctx->pend_gws == global_work_size && ctx->pend_n < k->pf_batch &&
         f == ctx->pend_f0 + ctx->pend_n && f != 0u && same_args(ctx, k)) {
         ++ctx->pend_n;  // the next frame of the run
-        return pending_error(ctx, RT_SUCCESS);
+        return RT_SUCCESS;
     }
     if (ctx->pend_k) {
         rc = rti::flush_frames(ctx);
@@ -953,7 +969,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     bool defer = false;
     if (n_frames == 1 && si == RT_SCHED_STEP && k->pf_defer) {
         defer = k->pf_defer == 1 ||
-                (k->pf_defer == 2 && k->pf_waits == ctx->host_waits && global_work_size >= k->pf_defer_min);
+                (k->pf_defer == 2 && k->pf_waits == ctx->host_waits && global_work_size >= k->pf_defer_min &&
+                 !ctx->mexposed && !ctx->dexposed);  // (a host that can synchronise outside the library)
         k->pf_waits = ctx->host_waits;
     }
     const bool fused = n_frames > 1 || wf || defer;
@@ -1271,6 +1288,10 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (!ea || !eb) return fail(RT_OUT_OF_RESOURCES);
             (void)hipEventRecord(ea, as);
         }
+        // (copy-engine gathers of the previous image read `out` in place: the accumulation that
+        // rewrites it comes after their copies)
+        e = rti::out_read_wait(ctx, as);
+        if (e != hipSuccess) return fail(map_hip(e));
 #ifndef RT_DIAG_NO_ACCUM  // diagnostic A/B builds only (wrong images): the render without its accumulation
         e = rtk::launch_accum_frames(a, k->math, k->accum_key, as);
         if (e != hipSuccess) return fail(map_hip(e));
@@ -1465,6 +1486,7 @@ int rtContextGetAccumStream(rt_context ctx, void** s) {
     if (!ctx) return RT_INVALID_CONTEXT;
     if (!s) return RT_INVALID_VALUE;
     if (!ctx->overlap) ctx->mexposed = true;  // the main stream leaves the library's view
+    ctx->dexposed = true;  // the caller may synchronise with the stream outside the library
     if (ctx->pend_k) (void)rti::flush_frames(ctx);
     *s = ctx->overlap ? ctx->astream : qs(ctx);
     return RT_SUCCESS;
@@ -1578,6 +1600,8 @@ int rtKernelForceGlobalScene(rt_kernel k, int force) {
 int rtBufferGetDevicePointer(rt_mem m, void** dptr) {
     if (!m || !dptr) return RT_INVALID_VALUE;
     if (m->ctx && m->ctx->pend_k) (void)rti::flush_frames(m->ctx);  // the caller may touch the bytes
+    // ... at any later time, after synchronising outside the library: no more frame coalescing
+    if (m->ctx) m->ctx->dexposed = true;
     *dptr = m->dptr;
     return RT_SUCCESS;
 }
@@ -1590,7 +1614,9 @@ int rtBufferGetSize(rt_mem m, size_t* size) {
 
 int rtContextGetStream(rt_context ctx, void** s) {
     if (!ctx || !s) return RT_INVALID_VALUE;
-    ctx->mexposed = true;  // the caller may enqueue there without going through the library
+    // the caller may enqueue there, or synchronise with it, without going through the library
+    // (qs below also launches any coalesced frames; none are held back from now on)
+    ctx->mexposed = true;
     *s = qs(ctx);
     return RT_SUCCESS;
 }

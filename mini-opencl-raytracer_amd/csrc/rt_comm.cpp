@@ -1,32 +1,37 @@
-// rt_comm.cpp -- multi-GPU band sharding + RCCL gather, behind include/rt_hip.h.
+// rt_comm.cpp -- multi-GPU band sharding + gather, behind include/rt_hip.h.
 //
 // The reference is single-device (CLRaytracer.cpp:104-120, one in-order queue CLutils.cpp:29).
 // A frame shards with no exchange until the image is needed, because every pixel's seed is
 // gid + HashUInt32(frameCount) over the GLOBAL work-item id (kernel_bvh.cl:445) and the gamma
 // accumulation is per pixel (:449-455).  Rank r renders the interleaved 8-row bands
-// b % nranks == r into its full-size output buffer (rtKernelSetRowInterleave); the gather then
-// moves each rank's bands, packed densely, to the root:
+// b % nranks == r into its full-size output buffer (rtKernelSetRowInterleave), at the rows they
+// occupy in the image; the gather moves them to the root.
 //
-//   context accumulation stream : [accumulate k] [pack k -> stage[s]]  [accumulate k+1] ...
-//   communicator stream         :                 (wait pack) [transfer k -> root slot s] [flag]
-//   root unpack stream          :                      (wait flags k) [unpack k -> dst] [free s]
-//   context render streams      : [render k+1 ........................................]
+// Copy-engine transport (default).  Every band is written by the copy engines (SDMA,
+// hipMemcpyDeviceToDeviceNoCU; over xGMI between GPUs) straight from the rank's `out` into the
+// same rows of the root's destination -- mapped into the rank by IPC handle (one ncclAllGather per
+// plan), or by address for ranks driven by one process.  No staging, no pack or unpack copy, no
+// compute unit anywhere: a persistent render holds every CU slot until it drains, and anything
+// that needs one -- RCCL's transfer kernel, the runtime's 2-D blit copies -- waits behind it
+// (profiles/r04/dist_flow_ab.txt).  Per gather k (seq within the plan):
 //
-// Two staging slots alternate, so step k's transfer runs under step k+1's render.
+//   sender accumulation stream : [accumulate k] (ready)                  [wait sent] [accumulate k+1]
+//   sender communicator stream :        (wait ready)(wait release k-1) [copies k] [arrive k] (sent)
+//   root unpack-stream         : (root's queue so far) [release k-1]   (wait arrive k from all) (gtail)
+//   render streams             : [render k+1 ..............................................]
 //
-// Transport (rtCommSetTransport).  A persistent render holds every CU slot until it drains, and
-// RCCL's transfer kernel (64 workgroups, 248 VGPRs, 37 KB LDS each on gfx950) fits beside it
-// nowhere: in the world-1 flow its transfer waited for renders to drain (19 ms for a 0.12-ms
-// copy) and every second step stalled on it (profiles/r04/dist_flow_ab.txt).  So by default the
-// bytes move on the COPY ENGINES (SDMA, hipMemcpyDeviceToDeviceNoCU; over xGMI between GPUs):
-// every rank copies its staging slot straight into the root's receive slot (an IPC-mapped
-// pointer to the root's memory, exchanged once per plan with one ncclAllGather), then raises its
-// arrival flag in the root's memory (hipStreamWriteValue64); the root's unpack stream waits for
-// the flags (hipStreamWaitValue64) and, after the unpack, raises each rank's slot-free flag,
-// which that rank's next copy into the slot waits for.  No compute unit is needed for the
-// transfer, no host round trip for the synchronisation.  RCCL stays for the setup, reductions
-// and barriers, and as the grouped ncclSend/ncclRecv transport (RT_COMM_TRANSPORT_RCCL; also
-// the fallback when a rank cannot map the root's memory).
+// `release k-1` (a flag in each sender's memory, or an event within one process) says the root
+// has enqueued gather k and everything it queued before (reads of image k-1) has run: a rank's
+// copies never change the root's image under a read.  `arrive k` (a flag per rank in the root's
+// memory) says the rank's bands of image k are in place; the root's context joins every arrival
+// before its next read (qs, gtail).  `sent` (the rank's copies done) orders the accumulation that
+// rewrites `out` after the copies that read it (rti::out_read_wait).
+//
+// RCCL transport (RT_COMM_TRANSPORT_RCCL, and the fallback of a world whose copy-engine links do
+// not hold): each rank packs its bands densely into a staging slot on its accumulation stream,
+// grouped ncclSend/ncclRecv move the slots to the root, the root unpacks them; two slots alternate
+// so step k's transfer runs under step k+1's render.  RCCL also carries the setup exchanges,
+// reductions and barriers.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,9 +40,11 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <dirent.h>
 #include <string>
 #include <thread>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "../../include/rt_hip.h"
@@ -50,6 +57,7 @@ namespace {
 
 constexpr unsigned kBandRows = 8;     // = the 8x8 tile height of the persistent schedules
 constexpr size_t kPixelBytes = 16;    // one float3 slot of the output buffer
+constexpr size_t kProbeBytes = 4096;  // per rank, the trial round's copy
 
 int map_nccl(ncclResult_t r) {
     switch (r) {
@@ -89,6 +97,21 @@ int band_plan(unsigned W, unsigned H, unsigned period, unsigned phase, rt_rect* 
     return RT_SUCCESS;
 }
 
+// The byte runs of the image one rank's bands occupy (adjacent bands merged: one run for a world of
+// one), in image order.
+std::vector<std::pair<uint64_t, uint64_t>> band_runs(const std::vector<rt_rect>& plan) {
+    std::vector<std::pair<uint64_t, uint64_t>> runs;
+    for (const rt_rect& r : plan)
+        for (uint64_t i = 0; i < r.rows; ++i) {
+            const uint64_t off = r.img_offset + i * r.img_pitch;
+            if (!runs.empty() && runs.back().first + runs.back().second == off)
+                runs.back().second += r.width;
+            else
+                runs.emplace_back(off, r.width);
+        }
+    return runs;
+}
+
 }  // namespace
 
 struct rt_comm_s {
@@ -97,40 +120,52 @@ struct rt_comm_s {
     // loopback worlds (rtCommInitLoopback): no RCCL; `group` identifies the world (shared by its
     // members), whose gathers always run on the copy engines with the members linked by address
     const void* group = nullptr;
-    hipEvent_t xfer = nullptr;  // (unused since the copy-engine transport; kept for the ABI of the struct's users)
     bool reserved = false;      // holds a CU reservation on ctx (rti::reserve_cus)
     int rank = 0, nranks = 1;
     hipStream_t cstream = nullptr;  // transfers (copy engines or RCCL), RCCL setup and reductions
-    hipStream_t ustream = nullptr;  // root: unpack
-    // gather buffers for one (width, height); rebuilt when the image size changes
+    hipStream_t ustream = nullptr;  // root: release / arrival waits (copy engines), unpack (RCCL)
+    // the plan: one (width, height, root, destination); rebuilt when any changes
     unsigned W = 0, H = 0;
     int root = -1;
-    size_t stage_bytes = 0;
-    std::vector<std::vector<rt_rect>> plans;  // per rank
-    void* stage[2] = {};                      // this rank's packed bands
-    void* parts[2] = {};                      // root: nranks x stage_bytes received bands
-    hipEvent_t packed[2] = {}, sent[2] = {}, unpacked[2] = {};
-    bool sent_valid[2] = {}, unpacked_valid[2] = {};
-    int slot = 0;
-    double* scratch = nullptr;  // reductions
-    // copy-engine transport (see the top of the file)
+    std::vector<std::vector<rt_rect>> plans;  // per rank: its bands as 2-D rects (rtBandPackPlan)
     int transport = RT_COMM_TRANSPORT_COPY_ENGINES;  // requested (rtCommSetTransport)
     bool ce = false;                 // this plan moves bytes on the copy engines
     bool ipc_linked = false;         // ... with its links exchanged as IPC handles (link_ipc)
+    int fallback_reason = RT_COMM_FALLBACK_NONE;  // the plan wanted the copy engines and runs RCCL
+    bool fail_links = false;         // test hook (RT_COMM_OPT_FAIL_LINKS)
     uint64_t seq = 0;                // gathers enqueued with this plan (1, 2, ...)
-    uint64_t* sflags = nullptr;      // [2] (fine-grained, this rank's memory): slot s freed by the root up to seq
-    uint64_t* rflags = nullptr;      // root, [nranks][2] (fine-grained): rank q's bytes for slot s arrived, seq
-    uint8_t* peer_parts[2] = {};     // the root's receive slots, as this rank addresses them
+    // ---- copy engines ----
+    rt_mem target = nullptr;         // root: the plan's destination (pinned)
+    uint8_t* peer_target = nullptr;  // the root's destination as this rank addresses it
+    std::vector<std::pair<uint64_t, uint64_t>> runs;  // this rank's band runs (image byte offset, bytes)
+    bool sends = false;              // this rank copies its bands (every rank but a root gathering into its out)
+    uint64_t* sflags = nullptr;      // [1] (fine-grained, this rank's memory): images released by the root, seq
+    uint64_t* rflags = nullptr;      // root, [nranks] (fine-grained): rank q's bands of image seq in place
+    uint8_t* probe = nullptr;        // root, [nranks][kProbeBytes] (fine-grained): the trial round's copies
+    uint8_t* peer_probe = nullptr;
     uint64_t* peer_rflags = nullptr; // the root's arrival flags, as this rank addresses them
-    std::vector<uint64_t*> peer_sflags;  // root: every rank's slot-free flags
+    std::vector<uint64_t*> peer_sflags;  // root: every rank's release flag
     std::vector<void*> ipc_opened;       // IPC mappings to close with the plan
-    // the copy-engine transfer split over streams of its own, which the runtime spreads over
-    // several SDMA engines (one engine: 61 GB/s; 2 streams 120, 8 streams 154 GB/s on MI355X,
+    hipEvent_t ready = nullptr;      // the bands of `out` are final (accumulation stream)
+    hipEvent_t sent = nullptr;       // this rank's copies of the last gather are done
+    hipEvent_t released = nullptr;   // root, one-process worlds: the previous image is released
+    hipEvent_t xt0 = nullptr, xt1 = nullptr;  // timing: the last gather's transfer on cstream
+    bool xt_valid = false;
+    // the copies split over streams of their own, which the runtime spreads over several SDMA
+    // engines (one engine: 61 GB/s; 2 streams 120, 8 streams 154 GB/s on MI355X,
     // scripts/probes/gather_engines_probe.hip split, profiles/r04/gather_engines_probe.txt).
     // Every stream shares the 4 hardware queues, though: in the world-1 flow 2 streams beat 1
     // (0.790 vs 0.798 ms/frame) and 8 stalled the renders (1.17; profiles/r04/dist_flow_ab.txt)
     hipStream_t xstream[8] = {};
     hipEvent_t xgo = nullptr, xdone[8] = {};
+    // ---- RCCL ----
+    size_t stage_bytes = 0;
+    void* stage[2] = {};                      // this rank's packed bands
+    void* parts[2] = {};                      // root: nranks x stage_bytes received bands
+    hipEvent_t packed[2] = {}, rsent[2] = {}, unpacked[2] = {};
+    bool rsent_valid[2] = {}, unpacked_valid[2] = {};
+    int slot = 0;
+    double* scratch = nullptr;  // reductions
     // shared worlds (rtCommInitShared): no RCCL; setup exchanges, reductions and barriers go
     // through files in `fdir` (exchange number fseq), the gathers over the copy engines
     std::string fdir;
@@ -182,7 +217,7 @@ int comm_streams(rt_comm c, bool rccl) {
 }
 
 #ifndef RT_COMM_XFER_STREAMS
-#define RT_COMM_XFER_STREAMS 2  // 1: the copy on the communicator stream itself
+#define RT_COMM_XFER_STREAMS 2  // 1: the copies on the communicator stream itself
 #endif
 #ifndef RT_COMM_XFER_PRIO
 #define RT_COMM_XFER_PRIO 1     // extra transfer streams at the greatest priority (own hardware queues)
@@ -196,13 +231,28 @@ int comm_events(rt_comm c, hipError_t e) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xdone[i], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xgo, hipEventDisableTiming);
+    for (hipEvent_t* ev : {&c->ready, &c->sent, &c->released})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&c->xt0);
+    if (e == hipSuccess) e = hipEventCreate(&c->xt1);
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipEventCreateWithFlags(&c->packed[s], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rsent[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->unpacked[s], hipEventDisableTiming);
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xfer, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64 * sizeof(double));
+    return map_hip(e);
+}
+
+// RCCL transport buffers: staging slots on every rank, receive slots on the root
+int rccl_buffers(rt_comm c) {
+    if (c->stage[0]) return RT_SUCCESS;
+    hipError_t e = hipSuccess;
+    for (int s = 0; s < 2 && e == hipSuccess; ++s) {
+        e = hipMalloc(&c->stage[s], std::max<size_t>(c->stage_bytes, 16));
+        if (e == hipSuccess && c->rank == c->root)
+            e = hipMalloc(&c->parts[s], std::max<size_t>(c->stage_bytes * c->nranks, 16));
+    }
     return map_hip(e);
 }
 
@@ -213,34 +263,44 @@ void free_buffers(rt_comm c) {
         if (c->stage[s]) (void)hipFree(c->stage[s]);
         if (c->parts[s]) (void)hipFree(c->parts[s]);
         c->stage[s] = c->parts[s] = nullptr;
-        c->peer_parts[s] = nullptr;
-        c->sent_valid[s] = c->unpacked_valid[s] = false;
+        c->rsent_valid[s] = c->unpacked_valid[s] = false;
     }
-    if (c->sflags) (void)hipFree(c->sflags);
-    if (c->rflags) (void)hipFree(c->rflags);
+    for (uint64_t** f : {&c->sflags, &c->rflags})
+        if (*f) (void)hipFree(*f);
+    if (c->probe) (void)hipFree(c->probe);
     c->sflags = c->rflags = c->peer_rflags = nullptr;
+    c->probe = c->peer_probe = c->peer_target = nullptr;
     c->peer_sflags.clear();
-    c->ce = c->ipc_linked = false;
+    if (c->target) rti::unpin(c->target);
+    c->target = nullptr;
+    c->runs.clear();
+    c->ce = c->ipc_linked = c->sends = false;
+    c->fallback_reason = RT_COMM_FALLBACK_NONE;
     c->seq = 0;
+    c->xt_valid = false;
+    c->slot = 0;
     c->W = c->H = 0;
     c->root = -1;
+    if (c->ctx->oread_ev == c->sent) c->ctx->oread = false;
 }
 
 void release(rt_comm c) {
     if (c->ctx) (void)hipSetDevice(c->ctx->device);
-    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
+    for (hipStream_t s : {c->cstream, c->ustream})
+        if (s) (void)hipStreamSynchronize(s);
+    for (hipStream_t s : c->xstream)
+        if (s) (void)hipStreamSynchronize(s);
     free_buffers(c);
+    if (c->ctx->oread_ev == c->sent) c->ctx->oread_ev = nullptr;
     for (int s = 0; s < 2; ++s)
-        for (hipEvent_t ev : {c->packed[s], c->sent[s], c->unpacked[s]})
+        for (hipEvent_t ev : {c->packed[s], c->rsent[s], c->unpacked[s]})
             if (ev) (void)hipEventDestroy(ev);
-    if (c->xfer) (void)hipEventDestroy(c->xfer);
+    for (hipEvent_t ev : {c->ready, c->sent, c->released, c->xt0, c->xt1, c->xgo})
+        if (ev) (void)hipEventDestroy(ev);
     for (int i = 0; i < 8; ++i) {
-        if (c->xstream[i]) (void)hipStreamSynchronize(c->xstream[i]);
         if (c->xstream[i]) (void)hipStreamDestroy(c->xstream[i]);
         if (c->xdone[i]) (void)hipEventDestroy(c->xdone[i]);
     }
-    if (c->xgo) (void)hipEventDestroy(c->xgo);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -255,14 +315,25 @@ void release(rt_comm c) {
     delete c;
 }
 
-// buffers and plans for a W x H gather (all earlier gathers of this comm have completed)
-int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, bool* built) {
+// Every stream of the communicator (and the context's accumulation stream, whose accumulations
+// a gather may follow) idle: a plan can be torn down.
+void quiesce(rt_comm c) {
+    for (hipStream_t s : {c->cstream, c->ustream, c->ctx->astream})
+        (void)hipStreamSynchronize(s);
+    for (hipStream_t s : c->xstream)
+        if (s) (void)hipStreamSynchronize(s);
+}
+
+// The plan of a W x H gather into `dst` (the root's destination; ranks other than the root pass
+// nullptr) from `out` -- all earlier gathers of this comm have completed when it is rebuilt.  A
+// copy-engine plan writes into the destination it was linked to, so a new one rebuilds it (the
+// RCCL transport unpacks into whatever the call names).
+int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, rt_mem dst, rt_mem out, bool* built) {
     *built = false;
-    if (c->W == W && c->H == H && c->root == root) return RT_SUCCESS;
+    if (c->W == W && c->H == H && c->root == root && (c->rank != root || !c->ce || dst == c->target))
+        return RT_SUCCESS;
     *built = true;
-    (void)hipStreamSynchronize(c->cstream);
-    (void)hipStreamSynchronize(c->ustream);
-    (void)hipStreamSynchronize(c->ctx->astream);
+    quiesce(c);
     free_buffers(c);
     c->plans.assign(c->nranks, {});
     size_t sb = 0;
@@ -274,43 +345,40 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, bool* built) {
         c->plans[q].assign(r, r + n);
     }
     c->stage_bytes = sb;
-    // copy engines: the root's receive slots and every flag word are fine-grained memory (the
-    // copies and flag writes come from other devices' engines; the unpack and the waits read
-    // them coherently), each its own allocation (an IPC handle maps a whole allocation)
-    const bool ce = c->transport != RT_COMM_TRANSPORT_RCCL;
-    auto alloc = [&](void** p, size_t n, bool fine) {
-        return fine ? hipExtMallocWithFlags(p, n, hipDeviceMallocFinegrained) : hipMalloc(p, n);
-    };
-    hipError_t e = hipSuccess;
-    for (int s = 0; s < 2 && e == hipSuccess; ++s) {
-        e = hipMalloc(&c->stage[s], std::max<size_t>(sb, 16));
-        if (e == hipSuccess && c->rank == root) e = alloc(&c->parts[s], std::max<size_t>(sb * c->nranks, 16), ce);
-    }
-    if (ce && e == hipSuccess) e = alloc(reinterpret_cast<void**>(&c->sflags), 2 * sizeof(uint64_t), true);
-    if (ce && e == hipSuccess && c->rank == root)
-        e = alloc(reinterpret_cast<void**>(&c->rflags), 2 * sizeof(uint64_t) * c->nranks, true);
-    if (ce && e == hipSuccess) e = hipMemset(c->sflags, 0, 2 * sizeof(uint64_t));
-    if (ce && e == hipSuccess && c->rflags) e = hipMemset(c->rflags, 0, 2 * sizeof(uint64_t) * c->nranks);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-        free_buffers(c);
-        return map_hip(e);
-    }
     c->W = W;
     c->H = H;
     c->root = root;
-    return RT_SUCCESS;
+    if (c->rank == root) {
+        c->target = dst;
+        rti::pin(dst);
+    }
+    // the root gathering into its own output has its bands in place already
+    c->sends = c->rank != root || dst != out;
+    if (c->transport == RT_COMM_TRANSPORT_RCCL) return rccl_buffers(c);
+    // copy engines: every flag word and the probe are fine-grained memory (written by other
+    // devices' engines, read coherently by the waits and the host), each its own allocation (an
+    // IPC handle maps a whole allocation)
+    c->runs = band_runs(c->plans[c->rank]);
+    hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sflags), sizeof(uint64_t), hipDeviceMallocFinegrained);
+    if (e == hipSuccess && c->rank == root)
+        e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->rflags), sizeof(uint64_t) * c->nranks,
+                                  hipDeviceMallocFinegrained);
+    if (e == hipSuccess && c->rank == root)
+        e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->probe), kProbeBytes * c->nranks, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) e = hipMemset(c->sflags, 0, sizeof(uint64_t));
+    if (e == hipSuccess && c->rflags) e = hipMemset(c->rflags, 0, sizeof(uint64_t) * c->nranks);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return map_hip(e);
 }
 
 // Copy-engine links of a plan whose members are all in this call (loopback worlds, and RCCL
-// worlds driven by one process): the root's slots and flags by address.  Between devices the
-// copy engines reach peer memory once peer access is on.
+// worlds driven by one process): the root's destination by address.  Between devices the copy
+// engines reach peer memory once peer access is on.
 int link_direct(const rt_comm* comms, int n_local, int root) {
     rt_comm R = nullptr;
     for (int i = 0; i < n_local; ++i)
         if (comms[i]->rank == root) R = comms[i];
     if (!R) return RT_INVALID_VALUE;
-    R->peer_sflags.assign(R->nranks, nullptr);
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         if (c->ctx->device != R->ctx->device) {
@@ -324,16 +392,16 @@ int link_direct(const rt_comm* comms, int n_local, int root) {
                 (void)hipGetLastError();
             }
         }
-        for (int s = 0; s < 2; ++s) c->peer_parts[s] = static_cast<uint8_t*>(R->parts[s]);
-        c->peer_rflags = R->rflags;
-        R->peer_sflags[c->rank] = c->sflags;
-        c->ce = true;
+    }
+    for (int i = 0; i < n_local; ++i) {
+        comms[i]->peer_target = static_cast<uint8_t*>(R->target->dptr);
+        comms[i]->ce = true;
     }
     return RT_SUCCESS;
 }
 
 // The same links across processes: every rank publishes IPC handles of its allocations (the
-// root: receive slots and arrival flags; everyone: slot-free flags) with one ncclAllGather, maps
+// root: destination, arrival flags and probe; everyone: release flag) with one ncclAllGather, maps
 // the ones it needs, and the world agrees (ncclAllReduce, max) whether every rank could -- if
 // one could not, the whole world keeps the RCCL transport for this plan.
 // Shared worlds: an all-gather of `n` bytes per rank through files -- each rank writes
@@ -388,7 +456,7 @@ int world_max(rt_comm c, int v, int* out) {
 }
 
 struct IpcBlob {
-    hipIpcMemHandle_t parts[2], rflags, sflags;
+    hipIpcMemHandle_t target, rflags, probe, sflags;
 };
 
 // the host waits for `s` until `deadline` (no hang: a stream stuck on a flag is reported)
@@ -402,12 +470,12 @@ bool wait_until(hipStream_t s, std::chrono::steady_clock::time_point deadline) {
 }
 
 // reads `n` u64 words of device memory until every word equals `v` or the deadline passes
-bool poll_words(const uint64_t* dev, size_t n, size_t stride, uint64_t v, std::chrono::steady_clock::time_point deadline) {
-    std::vector<uint64_t> h(n * stride);
+bool poll_words(const uint64_t* dev, size_t n, uint64_t v, std::chrono::steady_clock::time_point deadline) {
+    std::vector<uint64_t> h(n);
     for (;;) {
         if (hipMemcpy(h.data(), dev, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return false;
         bool all = true;
-        for (size_t i = 0; i < n; ++i) all &= h[i * stride] == v;
+        for (size_t i = 0; i < n; ++i) all &= h[i] == v;
         if (all) return true;
         if (std::chrono::steady_clock::now() > deadline) return false;
         std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -415,57 +483,61 @@ bool poll_words(const uint64_t* dev, size_t n, size_t stride, uint64_t v, std::c
 }
 
 // One trial round over fresh IPC links: every rank copies a 4-KB pattern into its part of the
-// root's slot 0 on the copy engines and raises its arrival flag; the root waits for every flag
+// root's probe on the copy engines and raises its arrival flag; the root waits for every flag
 // (from the host, then -- once they are in memory -- with the stream waits gathers use), checks
-// every pattern, raises every rank's slot-free flag; each rank waits for its own the same two
+// every pattern, raises every rank's release flag; each rank waits for its own the same two
 // ways; all flags go back to 0.  Returns 1 when anything failed or timed out.
 int ipc_handshake(rt_comm c) {
     constexpr uint64_t kMagic = 0x52545f4c494e4b31ull;
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(20);
-    const size_t n = std::min<size_t>(c->stage_bytes, 4096);
-    hipError_t e = hipMemsetAsync(c->stage[0], (c->rank + 1) & 0xff, n, c->cstream);
+    uint8_t* src = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&src), kProbeBytes);
+    if (e == hipSuccess) e = hipMemsetAsync(src, (c->rank + 1) & 0xff, kProbeBytes, c->cstream);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(c->peer_parts[0] + (size_t)c->rank * c->stage_bytes, c->stage[0], n,
+        e = hipMemcpyAsync(c->peer_probe + (size_t)c->rank * kProbeBytes, src, kProbeBytes,
                            hipMemcpyDeviceToDeviceNoCU, c->cstream);
-    if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank, kMagic, 0);
-    if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
+    if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + c->rank, kMagic, 0);
+    const bool sent_ok = e == hipSuccess && wait_until(c->cstream, deadline);
+    if (src) (void)hipFree(src);
+    if (!sent_ok) return 1;
     if (c->rank == c->root) {
-        if (!poll_words(c->rflags, (size_t)c->nranks, 2, kMagic, deadline)) return 1;
-        // the flags are in memory; the unpack stream's waits must see them too (the production path)
+        if (!poll_words(c->rflags, (size_t)c->nranks, kMagic, deadline)) return 1;
+        // the flags are in memory; the root stream's waits must see them too (the production path)
         for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-            e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q, kMagic, hipStreamWaitValueGte, ~0ull);
+            e = hipStreamWaitValue64(c->ustream, c->rflags + q, kMagic, hipStreamWaitValueGte, ~0ull);
         if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
-        std::vector<uint8_t> got(n);
+        std::vector<uint8_t> got(kProbeBytes);
         for (int q = 0; q < c->nranks; ++q) {
-            if (hipMemcpy(got.data(), static_cast<uint8_t*>(c->parts[0]) + (size_t)q * c->stage_bytes, n,
-                          hipMemcpyDeviceToHost) != hipSuccess)
+            if (hipMemcpy(got.data(), c->probe + (size_t)q * kProbeBytes, kProbeBytes, hipMemcpyDeviceToHost) != hipSuccess)
                 return 1;
             for (uint8_t b : got)
                 if (b != (uint8_t)((q + 1) & 0xff)) return 1;
         }
         for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
             e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q], kMagic, 0);
-        if (e == hipSuccess) e = hipMemsetAsync(c->rflags, 0, 2 * sizeof(uint64_t) * c->nranks, c->ustream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->rflags, 0, sizeof(uint64_t) * c->nranks, c->ustream);
         if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
     }
-    if (!poll_words(c->sflags, 1, 1, kMagic, deadline)) return 1;
+    if (!poll_words(c->sflags, 1, kMagic, deadline)) return 1;
     e = hipStreamWaitValue64(c->cstream, c->sflags, kMagic, hipStreamWaitValueGte, ~0ull);
     if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
-    e = hipMemset(c->sflags, 0, 2 * sizeof(uint64_t));
+    e = hipMemset(c->sflags, 0, sizeof(uint64_t));
     if (e == hipSuccess) e = hipDeviceSynchronize();
     return e == hipSuccess ? 0 : 1;
 }
+
 int link_ipc(rt_comm c) {
     hipError_t e = hipSetDevice(c->ctx->device);
     IpcBlob mine{};
-    int bad = 0;
+    // 0: links hold; RT_COMM_FALLBACK_IPC_MAP / _HANDSHAKE: why not (the world agrees on the max)
+    int bad = c->fail_links ? RT_COMM_FALLBACK_HANDSHAKE : 0;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.sflags, c->sflags);
     if (e == hipSuccess && c->rank == c->root) {
-        e = hipIpcGetMemHandle(&mine.parts[0], c->parts[0]);
-        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.parts[1], c->parts[1]);
+        e = hipIpcGetMemHandle(&mine.target, c->target->dptr);
         if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.rflags, c->rflags);
+        if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.probe, c->probe);
     }
-    if (e != hipSuccess) bad = 1;
+    if (e != hipSuccess) bad = std::max(bad, (int)RT_COMM_FALLBACK_IPC_MAP);
     std::vector<IpcBlob> all(c->nranks);
     auto exchange = [&]() -> int {
         if (!c->fdir.empty()) return file_allgather(c, &mine, sizeof(mine), all.data());
@@ -483,9 +555,10 @@ int link_ipc(rt_comm c) {
         return rc;
     };
     auto open = [&](const hipIpcMemHandle_t& h, void** p) {
+        *p = nullptr;
         if (bad) return;
         if (hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-            bad = 1;
+            bad = RT_COMM_FALLBACK_IPC_MAP;
             *p = nullptr;
             return;
         }
@@ -494,9 +567,9 @@ int link_ipc(rt_comm c) {
     int rc = exchange();
     if (!rc) {
         if (c->rank == c->root) {
-            c->peer_parts[0] = static_cast<uint8_t*>(c->parts[0]);
-            c->peer_parts[1] = static_cast<uint8_t*>(c->parts[1]);
+            c->peer_target = static_cast<uint8_t*>(c->target->dptr);
             c->peer_rflags = c->rflags;
+            c->peer_probe = c->probe;
             c->peer_sflags.assign(c->nranks, nullptr);
             for (int q = 0; q < c->nranks; ++q) {
                 if (q == c->rank) {
@@ -509,12 +582,12 @@ int link_ipc(rt_comm c) {
             }
         } else {
             void* p[3] = {};
-            open(all[c->root].parts[0], &p[0]);
-            open(all[c->root].parts[1], &p[1]);
-            open(all[c->root].rflags, &p[2]);
-            c->peer_parts[0] = static_cast<uint8_t*>(p[0]);
-            c->peer_parts[1] = static_cast<uint8_t*>(p[1]);
-            c->peer_rflags = static_cast<uint64_t*>(p[2]);
+            open(all[c->root].target, &p[0]);
+            open(all[c->root].rflags, &p[1]);
+            open(all[c->root].probe, &p[2]);
+            c->peer_target = static_cast<uint8_t*>(p[0]);
+            c->peer_rflags = static_cast<uint64_t*>(p[1]);
+            c->peer_probe = static_cast<uint8_t*>(p[2]);
         }
         // does every rank hold its links?
         rc = world_max(c, bad, &bad);
@@ -523,7 +596,7 @@ int link_ipc(rt_comm c) {
     // with a deadline, before any gather relies on them (a world whose first real gather waited on
     // a flag that never arrives would hang instead of falling back)
     if (!rc && !bad) {
-        bad = ipc_handshake(c);
+        bad = ipc_handshake(c) ? RT_COMM_FALLBACK_HANDSHAKE : 0;
         rc = world_max(c, bad, &bad);
     }
     if (rc) return rc;
@@ -531,28 +604,25 @@ int link_ipc(rt_comm c) {
     if (bad) {  // the world falls back to RCCL transfers for this plan
         for (void* p : c->ipc_opened) (void)hipIpcCloseMemHandle(p);
         c->ipc_opened.clear();
-        c->peer_parts[0] = c->peer_parts[1] = nullptr;
+        c->peer_target = c->peer_probe = nullptr;
         c->peer_rflags = nullptr;
         c->peer_sflags.clear();
         c->ce = false;
-        return RT_SUCCESS;
+        c->fallback_reason = bad;
+        return rccl_buffers(c);
     }
     c->ce = c->ipc_linked = true;
     return RT_SUCCESS;
 }
 
-// pack / unpack copies on the copy engines (hipMemcpyDeviceToDeviceNoCU) instead of blit kernels
-#ifndef RT_COMM_NOCU
-#define RT_COMM_NOCU 0
-#endif
+// pack / unpack copies of the RCCL transport (the runtime runs 2-D device copies as blit kernels)
 hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* stage, bool to_stage, hipStream_t s) {
-    const hipMemcpyKind kind = RT_COMM_NOCU ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
     for (const rt_rect& r : plan) {
         hipError_t e = to_stage
             ? hipMemcpy2DAsync(stage + r.stage_offset, r.width, img + r.img_offset, r.img_pitch, r.width, r.rows,
-                               kind, s)
+                               hipMemcpyDeviceToDevice, s)
             : hipMemcpy2DAsync(img + r.img_offset, r.img_pitch, stage + r.stage_offset, r.width, r.width, r.rows,
-                               kind, s);
+                               hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -560,9 +630,7 @@ hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* s
 
 int rccl_transfer(const rt_comm* comms, int n_local, int root);
 int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
-int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
-int link_direct(const rt_comm* comms, int n_local, int root);
-int link_ipc(rt_comm c);
+int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs);
 int check_loopback(const rt_comm* comms, int n_local);
 
 }  // namespace
@@ -682,6 +750,16 @@ int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_c
     *out = nullptr;
     if (!ctx) return RT_INVALID_CONTEXT;
     if (!dir || !*dir || nranks < 1 || rank < 0 || rank >= nranks) return RT_INVALID_VALUE;
+    // exchange files left by an earlier world would be read as this one's: refuse the directory
+    if (DIR* d = opendir(dir)) {
+        bool stale = false;
+        while (const dirent* ent = readdir(d))
+            stale |= ent->d_name[0] == 'x' && std::strstr(ent->d_name, "_r") != nullptr;
+        closedir(d);
+        if (stale) return RT_INVALID_VALUE;
+    } else {
+        return RT_FILE_NOT_FOUND;
+    }
     hipError_t he = hipSetDevice(ctx->device);
     if (he != hipSuccess) return map_hip(he);
     rt_comm c = new (std::nothrow) rt_comm_s();
@@ -726,13 +804,10 @@ int rtCommSetTransport(rt_comm c, int transport) {
         return RT_INVALID_VALUE;
     if (c->group && transport != RT_COMM_TRANSPORT_COPY_ENGINES) return RT_INVALID_OPERATION;
     if (!c->nc && transport == RT_COMM_TRANSPORT_RCCL) return RT_INVALID_OPERATION;  // shared worlds
-    if (transport == c->transport) return RT_SUCCESS;
     (void)hipSetDevice(c->ctx->device);
-    (void)hipStreamSynchronize(c->cstream);
-    (void)hipStreamSynchronize(c->ustream);
-    (void)hipStreamSynchronize(c->ctx->astream);
+    quiesce(c);
     c->transport = transport;
-    free_buffers(c);  // the next gather builds the plan for it
+    free_buffers(c);  // the next gather builds the plan for it (also: a new destination)
     return RT_SUCCESS;
 }
 
@@ -743,6 +818,39 @@ int rtCommGetTransport(rt_comm c, int* transport, int* active) {
     if (active) *active = c->W == 0 ? -1 : !c->ce ? RT_COMM_TRANSPORT_RCCL : c->ipc_linked ? RT_COMM_TRANSPORT_COPY_ENGINES_IPC
                                                                                    : RT_COMM_TRANSPORT_COPY_ENGINES;
     return RT_SUCCESS;
+}
+
+int rtCommGetStatus(rt_comm c, rt_comm_status* out) {
+    if (!c || !out) return RT_INVALID_VALUE;
+    std::memset(out, 0, sizeof(*out));
+    out->rank = c->rank;
+    out->nranks = c->nranks;
+    (void)rtCommGetTransport(c, &out->transport, &out->active);
+    out->fallback = c->fallback_reason != RT_COMM_FALLBACK_NONE;
+    out->fallback_reason = c->fallback_reason;
+    out->gathers = c->seq;
+    if (c->W != 0 && c->ce) {
+        if (c->sends)
+            for (const auto& r : c->runs) out->bytes_per_gather += r.second;
+        out->copies_per_gather = c->sends ? (unsigned)c->runs.size() : 0u;
+    } else if (c->W != 0) {
+        out->bytes_per_gather = c->stage_bytes;
+        out->copies_per_gather = 1;
+    }
+    out->last_xfer_ms = -1.0;
+    float ms = 0.0f;
+    if (c->xt_valid && hipEventQuery(c->xt1) == hipSuccess && hipEventElapsedTime(&ms, c->xt0, c->xt1) == hipSuccess)
+        out->last_xfer_ms = ms;
+    return RT_SUCCESS;
+}
+
+int rtCommSetOption(rt_comm c, int option, int value) {
+    if (!c) return RT_INVALID_VALUE;
+    if (option == RT_COMM_OPT_FAIL_LINKS) {
+        c->fail_links = value != 0;
+        return RT_SUCCESS;
+    }
+    return RT_INVALID_VALUE;
 }
 
 int rtCommShardKernel(rt_comm c, rt_kernel k) {
@@ -756,22 +864,30 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     const uint64_t img_bytes = (uint64_t)W * H * kPixelBytes;
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
-        if (!c || !outs[i]) return RT_INVALID_VALUE;
+        if (!c || !outs[i] || outs[i]->released) return RT_INVALID_VALUE;
         if (root < 0 || root >= c->nranks) return RT_INVALID_VALUE;
         if (outs[i]->ctx != c->ctx || outs[i]->size < img_bytes) return RT_INVALID_MEM_OBJECT;
-        if (c->rank == root && root_dst && (root_dst->ctx != c->ctx || root_dst->size < img_bytes))
+        if (c->rank == root && root_dst &&
+            (root_dst->released || root_dst->ctx != c->ctx || root_dst->size < img_bytes))
             return RT_INVALID_MEM_OBJECT;
     }
     if (int rc = check_loopback(comms, n_local)) return rc;
     for (int i = 0; i < n_local; ++i)  // coalesced per-frame launches first: the gather reads their output
         if (comms[i]->ctx->pend_k) (void)rti::flush_frames(comms[i]->ctx);
-    // the plans (rebuilt, by every rank alike, when the size, the root or the transport changes)
+    // the plans (rebuilt, by every rank alike, when the size, the root or the transport changes).
+    // The root's destination is part of the plan: when every rank is in this call a new one
+    // rebuilds it too; a rank alone in its process cannot tell the others, so its root refuses it
+    const bool whole_world = n_local == comms[0]->nranks;
     bool fresh = false;
     for (int i = 0; i < n_local; ++i) {
-        hipError_t e = hipSetDevice(comms[i]->ctx->device);
+        rt_comm c = comms[i];
+        hipError_t e = hipSetDevice(c->ctx->device);
         if (e != hipSuccess) return map_hip(e);
+        rt_mem dst = c->rank == root ? (root_dst ? root_dst : outs[i]) : nullptr;
+        if (!whole_world && c->rank == root && c->W == W && c->H == H && c->root == root && c->ce && c->target != dst)
+            return RT_INVALID_OPERATION;
         bool built = false;
-        int rc = ensure_plan(comms[i], W, H, root, &built);
+        int rc = ensure_plan(c, W, H, root, dst, outs[i], &built);
         if (rc) return rc;
         fresh |= built;
     }
@@ -780,11 +896,15 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         if (comms[0]->transport == RT_COMM_TRANSPORT_COPY_ENGINES_IPC) {
             if (n_local != 1 || (!comms[0]->nc && comms[0]->fdir.empty())) return RT_INVALID_OPERATION;
             rc = link_ipc(comms[0]);
-        } else if (n_local == comms[0]->nranks) {
+        } else if (whole_world) {
             rc = link_direct(comms, n_local, root);  // every member is in this call
             if (rc && !comms[0]->group) {            // (RCCL world: keep RCCL's transfers)
-                for (int i = 0; i < n_local; ++i) comms[i]->ce = false;
                 rc = RT_SUCCESS;
+                for (int i = 0; i < n_local && !rc; ++i) {
+                    comms[i]->ce = false;
+                    comms[i]->fallback_reason = RT_COMM_FALLBACK_NO_PEER_ACCESS;
+                    rc = rccl_buffers(comms[i]);
+                }
             }
         } else if (n_local == 1 && (comms[0]->nc || !comms[0]->fdir.empty())) {
             rc = link_ipc(comms[0]);
@@ -795,7 +915,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     for (int i = 0; i < n_local; ++i) ce &= comms[i]->ce;
     // loopback and shared worlds move bytes on the copy engines only
     if ((comms[0]->group || !comms[0]->fdir.empty()) && !ce) return RT_INVALID_OPERATION;
-    if (ce) return ce_gather(comms, n_local, root, root_dst, outs);
+    if (ce) return ce_gather(comms, n_local, root, outs);
     // RCCL transport.  Phase 1: every rank (the root too) packs its bands on its context's
     // accumulation stream
     for (int i = 0; i < n_local; ++i) {
@@ -803,12 +923,14 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         rt_context ctx = c->ctx;
         hipError_t e = hipSetDevice(ctx->device);
         if (e != hipSuccess) return map_hip(e);
+        if (int rc = rccl_buffers(c)) return rc;
         const int s = c->slot;
+        ++c->seq;
         uint8_t* out = static_cast<uint8_t*>(outs[i]->dptr);
         // the bands are final after every accumulation enqueued so far (astream, in order) and
         // after whatever the main stream has queued (per-frame launches write `out` there)
         e = rti::main_tail_wait(ctx, ctx->astream);
-        if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);  // slot free
+        if (e == hipSuccess && c->rsent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->rsent[s], 0);  // slot free
         if (e == hipSuccess)
             e = copy_rects(c->plans[c->rank], out, static_cast<uint8_t*>(c->stage[s]), true, ctx->astream);
         if (e == hipSuccess) e = hipEventRecord(c->packed[s], ctx->astream);
@@ -816,6 +938,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         if (e == hipSuccess && c->rank == root && c->unpacked_valid[s])
             e = hipStreamWaitEvent(c->cstream, c->unpacked[s], 0);  // receive slot's last unpack done
         if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
+        if (e == hipSuccess) e = hipEventRecord(c->xt0, c->cstream);
         if (e != hipSuccess) return map_hip(e);
         ctx->apending = true;
     }
@@ -849,22 +972,42 @@ int rccl_transfer(const rt_comm* comms, int n_local, int root) {
     return rc_end;
 }
 
-// `n` bytes on the copy engines, after and before everything on the communicator stream:
-// chunks of at least 1 MiB over the transfer streams (several ranks driven by one process share
-// its hardware queues, so they copy on the one stream)
-hipError_t copy_engines(rt_comm c, uint8_t* dst, const uint8_t* src, size_t n) {
+// The rank's band runs on the copy engines, after and before everything on the communicator
+// stream: the bytes dealt out over the transfer streams in image order, in pieces of at least
+// 1 MiB (several ranks driven by one process share its hardware queues, so they copy on the one
+// stream).  The destination is the root's image (or, for a root gathering into another buffer,
+// that buffer) at the same offsets.
+hipError_t copy_bands(rt_comm c, const uint8_t* src) {
+    uint64_t total = 0;
+    for (const auto& r : c->runs) total += r.second;
     const bool shared = !c->ipc_linked && c->nranks > 1;
-    const size_t k = shared ? 1 : std::max<size_t>(1, std::min<size_t>(RT_COMM_XFER_STREAMS, n >> 20));
-    if (k == 1) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, c->cstream);
-    const size_t chunk = ((n + k - 1) / k + 255) & ~(size_t)255;
+    const size_t k = shared ? 1 : std::max<size_t>(1, std::min<uint64_t>(RT_COMM_XFER_STREAMS, total >> 20));
+    auto copy = [&](uint64_t off, uint64_t n, hipStream_t s) {
+        return hipMemcpyAsync(c->peer_target + off, src + off, n, hipMemcpyDeviceToDeviceNoCU, s);
+    };
+    if (k == 1) {
+        for (const auto& r : c->runs)
+            if (hipError_t e = copy(r.first, r.second, c->cstream)) return e;
+        return hipSuccess;
+    }
     hipError_t e = hipEventRecord(c->xgo, c->cstream);
-    for (size_t i = 0; i < k && e == hipSuccess; ++i) {
-        const size_t off = i * chunk;
-        if (off >= n) break;
+    const uint64_t share = ((total + k - 1) / k + 255) & ~(uint64_t)255;
+    size_t run = 0;
+    uint64_t run_done = 0;  // bytes of runs[run] already dealt out
+    for (size_t i = 0; i < k && e == hipSuccess && run < c->runs.size(); ++i) {
         e = hipStreamWaitEvent(c->xstream[i], c->xgo, 0);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(dst + off, src + off, std::min(chunk, n - off), hipMemcpyDeviceToDeviceNoCU,
-                               c->xstream[i]);
+        uint64_t left = share;
+        while (e == hipSuccess && left > 0 && run < c->runs.size()) {
+            const auto& r = c->runs[run];
+            const uint64_t n = std::min(left, r.second - run_done);
+            e = copy(r.first + run_done, n, c->xstream[i]);
+            left -= n;
+            run_done += n;
+            if (run_done == r.second) {
+                ++run;
+                run_done = 0;
+            }
+        }
         if (e == hipSuccess) e = hipEventRecord(c->xdone[i], c->xstream[i]);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->xdone[i], 0);
     }
@@ -872,101 +1015,89 @@ hipError_t copy_engines(rt_comm c, uint8_t* dst, const uint8_t* src, size_t n) {
 }
 
 // Copy-engine gather (see the top of the file).  Between processes (IPC links), flags carry the
-// gather's sequence number seq (1, 2, ... within a plan): rflags[q][s] = seq when rank q's bytes
-// for slot s have landed in the root's receive slot, sflags[s] = seq when the root has unpacked
-// slot s -- the next copy into that slot (gather seq + 2) waits for it.  Ranks driven by this
-// process (loopback worlds, rtCommInitAll) order the same steps with events instead (the
-// sender's `sent`, the root's `unpacked`): no waiting kernel on a hardware queue their other
-// streams share.  Gathering into the root's own output, its own bands are in place: it neither
-// packs nor sends them.
-int ce_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs) {
+// gather's sequence number seq (1, 2, ... within a plan): rflags[q] = seq when rank q's bands of
+// image seq are in the root's destination, sflags = seq when the root has released image seq (its
+// reads of it are done) -- a rank's copies of image seq + 1 wait for it.  Ranks driven by this
+// process (loopback worlds, rtCommInitAll) order the same steps with events instead (the root's
+// `released`, the senders' `sent`): no waiting packet on a hardware queue their other streams
+// share.
+int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
     rt_comm R = nullptr;  // the root, when it is driven by this call
     for (int i = 0; i < n_local; ++i)
         if (comms[i]->rank == root) R = comms[i];
-    for (int i = 0; i < n_local; ++i) {
-        rt_comm c = comms[i];
-        rt_context ctx = c->ctx;
-        const int s = c->slot;
-        const uint64_t seq = ++c->seq;
-        const bool into_out = c->rank == root && (!root_dst || root_dst == outs[i]);
-        hipError_t e = hipSetDevice(ctx->device);
-        if (e == hipSuccess && !into_out) {
-            // pack on the accumulation stream, after the accumulations (and main-stream work)
-            // that write `out`, once the copy engine has read the slot's previous contents
-            e = rti::main_tail_wait(ctx, ctx->astream);
-            if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);
-            if (e == hipSuccess)
-                e = copy_rects(c->plans[c->rank], static_cast<uint8_t*>(outs[i]->dptr),
-                               static_cast<uint8_t*>(c->stage[s]), true, ctx->astream);
-            if (e == hipSuccess) e = hipEventRecord(c->packed[s], ctx->astream);
-            if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
-            if (e == hipSuccess) ctx->apending = true;
-            // transfer on the communicator stream: into the root's slot once the root has
-            // unpacked what the slot held two gathers ago, then the arrival flag
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->packed[s], 0);
-            if (c->ipc_linked) {
-                if (e == hipSuccess && seq > 2)
-                    e = hipStreamWaitValue64(c->cstream, c->sflags + s, seq - 2, hipStreamWaitValueGte, ~0ull);
-            } else if (e == hipSuccess && R->unpacked_valid[s]) {
-                e = hipStreamWaitEvent(c->cstream, R->unpacked[s], 0);
-            }
-            if (e == hipSuccess) e = copy_engines(c, c->peer_parts[s] + (size_t)c->rank * c->stage_bytes,
-                                                  static_cast<const uint8_t*>(c->stage[s]), c->stage_bytes);
-            if (e == hipSuccess && c->ipc_linked)
-                e = hipStreamWriteValue64(c->cstream, c->peer_rflags + 2 * c->rank + s, seq, 0);
-            if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
-            if (e == hipSuccess) c->sent_valid[s] = true;
-        }
+    // 1. the root releases the previous image once everything its context queued so far has run
+    if (R) {
+        hipError_t e = hipSetDevice(R->ctx->device);
+        const uint64_t prev = R->seq;
+        if (e == hipSuccess) e = rti::main_tail_wait(R->ctx, R->ustream);
+        // (reads on the accumulation stream: rtContextSetReadbackOnAccumStream)
+        if (e == hipSuccess && R->ctx->readback_on_astream) e = hipStreamWaitEvent(R->ustream, R->ctx->atail, 0);
+        for (int q = 0; R->ipc_linked && prev > 0 && q < R->nranks && e == hipSuccess; ++q)
+            if (q != root || R->sends) e = hipStreamWriteValue64(R->ustream, R->peer_sflags[q], prev, 0);
+        if (e == hipSuccess && !R->ipc_linked) e = hipEventRecord(R->released, R->ustream);
         if (e != hipSuccess) return map_hip(e);
     }
+    // 2. every sending rank copies its bands of `out` into the root's destination
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         rt_context ctx = c->ctx;
-        const int s = c->slot;
-        const uint64_t seq = c->seq;
+        const uint64_t seq = ++c->seq;
         hipError_t e = hipSetDevice(ctx->device);
-        hipStream_t tail = c->cstream;
-        if (e == hipSuccess && c->rank == root) {
-            // the root: wait for every sender's bytes, unpack them, free the slot for each sender
-            const bool into_out = !root_dst || root_dst == outs[i];
-            uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
-            if (c->ipc_linked) {
-                for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-                    if (!(into_out && q == c->rank))
-                        e = hipStreamWaitValue64(c->ustream, c->rflags + 2 * q + s, seq, hipStreamWaitValueGte, ~0ull);
-            } else {
-                for (int j = 0; j < n_local && e == hipSuccess; ++j)
-                    if (!(into_out && comms[j] == c)) e = hipStreamWaitEvent(c->ustream, comms[j]->sent[s], 0);
+        if (e == hipSuccess && c->sends) {
+            // the bands are final after the accumulations (astream) and the per-frame launches
+            // (main stream) queued so far
+            e = rti::main_tail_wait(ctx, ctx->astream);
+            if (e == hipSuccess) e = hipEventRecord(c->ready, ctx->astream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->ready, 0);
+            if (e == hipSuccess && seq > 1) {  // the root is done with the previous image
+                e = c->ipc_linked ? hipStreamWaitValue64(c->cstream, c->sflags, seq - 1, hipStreamWaitValueGte, ~0ull)
+                                  : hipStreamWaitEvent(c->cstream, R->released, 0);
             }
-            for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-                if (!(into_out && q == c->rank))
-                    e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
-                                   false, c->ustream);
-            for (int q = 0; c->ipc_linked && q < c->nranks && e == hipSuccess; ++q)
-                if (!(into_out && q == c->rank)) e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q] + s, seq, 0);
-            if (e == hipSuccess) e = hipEventRecord(c->unpacked[s], c->ustream);
-            if (e == hipSuccess) c->unpacked_valid[s] = true;
-            tail = c->ustream;
+            if (e == hipSuccess) e = hipEventRecord(c->xt0, c->cstream);
+            if (e == hipSuccess) e = copy_bands(c, static_cast<const uint8_t*>(outs[i]->dptr));
+            if (e == hipSuccess) e = hipEventRecord(c->xt1, c->cstream);
+            if (e == hipSuccess && c->ipc_linked)
+                e = hipStreamWriteValue64(c->cstream, c->peer_rflags + c->rank, seq, 0);
+            if (e == hipSuccess) e = hipEventRecord(c->sent, c->cstream);
+            if (e == hipSuccess) {
+                c->xt_valid = true;
+                // the accumulation that next rewrites `out` waits for these copies
+                ctx->oread_ev = c->sent;
+                ctx->oread = true;
+            }
         }
-        // reads on this context wait for its part of the gather (qs)
-        if (e == hipSuccess) e = hipEventRecord(ctx->gtail, tail);
+        // reads on a sender's context wait for its copies (qs)
+        if (e == hipSuccess && c != R) e = hipEventRecord(ctx->gtail, c->cstream);
         if (e != hipSuccess) return map_hip(e);
-        ctx->gpending = true;
-        c->slot ^= 1;
+        if (c != R) ctx->gpending = true;
+    }
+    // 3. the root's context joins every rank's arrival
+    if (R) {
+        hipError_t e = hipSetDevice(R->ctx->device);
+        const uint64_t seq = R->seq;
+        for (int q = 0; R->ipc_linked && q < R->nranks && e == hipSuccess; ++q)
+            if (q != root || R->sends) e = hipStreamWaitValue64(R->ustream, R->rflags + q, seq, hipStreamWaitValueGte, ~0ull);
+        for (int j = 0; !R->ipc_linked && j < n_local && e == hipSuccess; ++j)
+            if (comms[j]->sends) e = hipStreamWaitEvent(R->ustream, comms[j]->sent, 0);
+        if (e == hipSuccess) e = hipEventRecord(R->ctx->gtail, R->ustream);
+        if (e != hipSuccess) return map_hip(e);
+        R->ctx->gpending = true;
     }
     return RT_SUCCESS;
 }
 
-// phase 3: the root unpacks every rank's bands into the destination
+// phase 3 of the RCCL transport: the root unpacks every rank's bands into the destination
 int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs) {
     for (int i = 0; i < n_local; ++i) {
         rt_comm c = comms[i];
         rt_context ctx = c->ctx;
         const int s = c->slot;
         hipError_t e = hipSetDevice(ctx->device);
-        if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
+        if (e == hipSuccess) e = hipEventRecord(c->xt1, c->cstream);
+        if (e == hipSuccess) e = hipEventRecord(c->rsent[s], c->cstream);
         if (e != hipSuccess) return map_hip(e);
-        c->sent_valid[s] = true;
+        c->xt_valid = true;
+        c->rsent_valid[s] = true;
         if (c->rank == root) {
             // Gathering into the root's own output: its own bands are in place already and are
             // not unpacked, so the unpack writes only other ranks' rows, which no later render,
@@ -975,10 +1106,12 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
             // accumulation, and the render after it, to the transfer: RCCL's kernel gets CUs only
             // as a persistent render drains, so every second render started a step late --
             // world-1 0.90 vs 0.77 ms/frame, profiles/r04/dist_flow_ab.txt.)  Reads of the
-            // image wait for it through the context's queue (gtail, qs()).
+            // image wait for it through the context's queue (gtail, qs()); the unpack waits for
+            // the reads queued before this gather.
             const bool into_out = !root_dst || root_dst == outs[i];
             uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
-            e = hipStreamWaitEvent(c->ustream, c->sent[s], 0);
+            e = rti::main_tail_wait(ctx, c->ustream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->ustream, c->rsent[s], 0);
             for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
                 if (!(into_out && q == c->rank))
                     e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
@@ -1096,8 +1229,8 @@ int rtCommBarrier(const rt_comm* comms, int n_local) {
     return rtCommAllReduceF64(comms, n_local, v.data(), 1, RT_COMM_SUM);
 }
 
-int rtBandPackPlan(unsigned width, unsigned height, unsigned period, unsigned phase, rt_rect* rects, int capacity,
-                   int* n_rects, size_t* staging_bytes) {
+int rtBandPackPlan(unsigned width, unsigned height, unsigned period, unsigned phase, rt_rect* rects,
+                   int capacity, int* n_rects, size_t* staging_bytes) {
     return band_plan(width, height, period, phase, rects, capacity, n_rects, staging_bytes);
 }
 

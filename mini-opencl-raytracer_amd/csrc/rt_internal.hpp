@@ -46,6 +46,9 @@ struct rt_context_s {
     // (rtContextGetStream), since the caller may then enqueue without telling us.
     bool mdirty = true;
     bool mexposed = false;
+    // a device pointer of one of the context's buffers, or its accumulation stream, was handed out:
+    // the host may synchronise outside the library, so per-frame launches are no longer coalesced
+    bool dexposed = false;
     bool apending = false;
     // host waits on the queue (rtFinish, blocking reads / writes): a per-frame launch with no wait
     // since the previous one is being queued back to back (automatic per-frame deferral)
@@ -58,6 +61,10 @@ struct rt_context_s {
     // the accumulations, so reads of the gathered image are ordered after it
     hipEvent_t gtail = nullptr;
     bool gpending = false;
+    // copy-engine gathers read the output buffer in place (rt_comm.cpp ce_gather): the next
+    // accumulation -- which rewrites it -- waits for their copies (oread_ev, the comm's `sent`)
+    hipEvent_t oread_ev = nullptr;
+    bool oread = false;
     // per-frame launches queued back to back and not launched yet (rt_capi.cpp, frame
     // coalescing): frames pend_f0 .. pend_f0 + pend_n - 1 of pend_k with the arguments they were
     // enqueued with; launched as one fused launch before anything else touches the context
@@ -79,6 +86,10 @@ struct rt_mem_s {
     std::vector<uint8_t> shadow;  // host copy of the bytes (valid when shadow_valid)
     bool shadow_valid = false;
     uint64_t generation = 0;      // bumped on every host write
+    // a copy-engine gather plan writes into this buffer (the root's destination, rt_comm.cpp):
+    // rtReleaseBuffer then only marks it, and the plan frees it when it lets go (rti::unpin)
+    int pins = 0;
+    bool released = false;
 };
 
 namespace rti {
@@ -128,6 +139,17 @@ inline hipError_t main_tail_wait(rt_context ctx, hipStream_t s) {
     }
     return hipStreamWaitEvent(s, ctx->mtail, 0);
 }
+
+// the next accumulation launch on `s` rewrites the output: after the gathers reading it in place
+inline hipError_t out_read_wait(rt_context ctx, hipStream_t s) {
+    if (!ctx->oread) return hipSuccess;
+    ctx->oread = false;
+    return hipStreamWaitEvent(s, ctx->oread_ev, 0);
+}
+
+// Gather destinations (rt_mem_s::pins): a pinned buffer outlives rtReleaseBuffer until unpinned.
+inline void pin(rt_mem m) { ++m->pins; }
+void unpin(rt_mem m);  // rt_capi.cpp: frees a released buffer on its last unpin
 
 // rtCommShardKernel's interleave (rt_capi.cpp): refused for a kernel with a work range
 int shard_kernel(rt_kernel k, unsigned period, unsigned phase);

@@ -1,5 +1,6 @@
 // image.cpp -- output/format step (include/rt_image.h): accumulation buffer -> PPM / PNG.
 #include <cstdint>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -167,7 +168,12 @@ extern "C" int rtiLoadAccum(const char* path, float* px, unsigned* W, unsigned* 
     if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kAccumMagic, 8) != 0 ||
         std::fread(hdr, sizeof(hdr), 1, f) != 1 || hdr[0] == 0 || hdr[1] == 0)
         rc = RT_PARSE_ERROR;
-    const size_t bytes = rc ? 0 : (size_t)hdr[0] * hdr[1] * 16;
+    // W * H * 16 bytes must not wrap (a crafted W = H = 2^30 would make it 0 and let a 28-byte file
+    // through, then a caller sizing W * H * 16 itself overflows too), and must fit a file offset
+    size_t bytes = 0;
+    if (!rc && (__builtin_mul_overflow((size_t)hdr[0], (size_t)hdr[1], &bytes) ||
+                __builtin_mul_overflow(bytes, (size_t)16, &bytes) || bytes > (size_t)LONG_MAX - 64))
+        rc = RT_PARSE_ERROR;
     if (!rc) {
         // the file holds exactly header + pixels + checksum
         if (std::fseek(f, 0, SEEK_END) != 0 || std::ftell(f) != (long)(8 + sizeof(hdr) + bytes + 8) ||

@@ -47,7 +47,7 @@ class HipRenderer:
     """One context + kernel + scene + output buffer; frames rendered on demand."""
 
     def __init__(self, scene, width, height, math=N.MATH_PINNED, device=0, hits=False,
-                 stats=False, force_global=False, global_size=None, sched=N.SCHED_STEP):
+                 stats=False, force_global=False, global_size=None, sched=N.SCHED_STEP, perframe_batch=1):
         self.W, self.H = width, height
         self.n = global_size if global_size is not None else width * height
         self.ctx = clrt.CLContext(device)
@@ -66,6 +66,11 @@ class HipRenderer:
         self.k.set_schedule(sched)
         self.k.force_global_scene(force_global)
         self.k.set_stats(stats)
+        # per-frame launches launch one by one (the per-frame baselines the tests compare against);
+        # frame coalescing is the subject only where a test asks for it (perframe_batch > 1, or
+        # None: the library default)
+        if perframe_batch is not None:
+            self.k.set_tuning("perframe_batch", perframe_batch)
         self.hit_bufs = None
         if hits:
             self.hit_bufs = (self.ctx.create_buffer(N.MEM_READ_WRITE, self.n * 4),

@@ -231,6 +231,18 @@ void checkpoints() {
     std::vector<float> small(4 * 2 * 2);
     if (rtiLoadAccum(path.c_str(), small.data(), &w, &h, &f) == RT_SUCCESS && (w != W || h != H)) std::abort();
     if (rtiLoadAccum((g_dir + "/missing.bin").c_str(), nullptr, &w, &h, &f) == RT_SUCCESS) std::abort();
+    // a crafted header whose W * H * 16 wraps to 0 (W = H = 2^30) over a header-only file: refused,
+    // header-only read included (a caller would size W * H * 16 from it)
+    {
+        std::vector<unsigned char> b(bytes.begin(), bytes.begin() + 8);
+        const uint32_t hdr[3] = {1u << 30, 1u << 30, 1u};
+        b.insert(b.end(), reinterpret_cast<const unsigned char*>(hdr), reinterpret_cast<const unsigned char*>(hdr) + 12);
+        b.insert(b.end(), 8, 0);
+        write(b);
+        if (rtiLoadAccum(bad.c_str(), nullptr, &w, &h, &f) == RT_SUCCESS) std::abort();
+        if (rtiLoadAccum(bad.c_str(), back.data(), &w, &h, &f) == RT_SUCCESS) std::abort();
+        ++g_rejected;
+    }
 }
 
 int main(int argc, char** argv) {

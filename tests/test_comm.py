@@ -12,6 +12,7 @@ rank its own context, the RCCL transfer replaced by device copies, the rest of t
 at the bench's full 4K 8-spp size; the RCCL transfer between N > 1 GPUs is the driver's 8-GPU
 bench.  The band arithmetic is also the CPU part here and tests/test_multigpu_gloo.py.
 """
+import json
 import os
 import subprocess
 import sys
@@ -103,11 +104,11 @@ def _read(ctx, buf, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["copy", "rccl", "copy-ipc"])
-@pytest.mark.parametrize("init,into_out", [("rank", False), ("rank", True), ("all", False)])
+@pytest.mark.parametrize("init,into_out,transport",
+                         [(i, o, t) for i, o in (("rank", False), ("rank", True), ("all", False))
+                          for t in ("copy", "rccl", "copy-ipc")
+                          if not (i == "all" and t == "copy-ipc")])  # (IPC links: one process per GPU)
 def test_gather_world_of_one(cornell, init, into_out, transport):
-    if transport == "copy-ipc" and init == "all":
-        pytest.skip("the IPC links are the one-process-per-GPU setup's")
     import clrt
     W, H = 640, 360
     ctx = clrt.CLContext(0)
@@ -145,6 +146,115 @@ def test_gather_world_of_one(cornell, init, into_out, transport):
         b.release()
     k.release()
     k2.release()
+    ctx.release()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["copy", "copy-ipc"])
+def test_gather_images_read_by_kernels_are_current(cornell, transport):
+    """The copy engines write the root's image behind the GPU caches' back (SDMA, from another
+    device's engine between GPUs): a kernel that reads the image after each gather -- here the
+    runtime's 2-D blit copy, an L2-cached read of an image small enough to stay in L2 from one
+    step to the next -- must see that gather's bytes, never the previous step's lines."""
+    import clrt
+    W, H, steps = 256, 144, 6
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES if transport == "copy" else N.COMM_TRANSPORT_COPY_ENGINES_IPC)
+    bufs, out, k = _setup(ctx, cornell, W, H)
+    comm.shard(k)
+    dst = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    snaps = [ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16) for _ in range(steps)]
+    for step in range(steps):
+        k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+        ctx.ExecuteKernelFrames(k, W * H, 8)
+        mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=dst)
+        ctx.CopyRectToDevicePointer(dst, 0, W * 16, W * 16, H, snaps[step].device_pointer(), W * 16)
+    ctx.Finish()
+    got = [_read(ctx, s, W * H) for s in snaps]
+    bufs2, out2, k2 = _setup(ctx, cornell, W, H)
+    for step in range(steps):
+        k2.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+        ctx.ExecuteKernelFrames(k2, W * H, 8)
+        assert got[step].tobytes() == _read(ctx, out2, W * H).tobytes(), f"step {step}: stale or torn image"
+    comm.destroy()
+    for b in bufs + bufs2 + [out, out2, dst] + snaps:
+        b.release()
+    k.release()
+    k2.release()
+    ctx.release()
+
+
+@pytest.mark.gpu
+def test_gather_forced_link_failure_falls_back_to_rccl(cornell):
+    """A world whose copy-engine links fail (the test hook makes this rank report them broken at
+    the link step) falls back to RCCL transfers for the plan, says so in its status, and gathers
+    the same bytes."""
+    import clrt
+    W, H = 640, 360
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES_IPC)
+    comm.set_option(N.COMM_OPT_FAIL_LINKS, 1)
+    bufs, out, k = _setup(ctx, cornell, W, H)
+    comm.shard(k)
+    dst = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    for step in range(3):
+        k.set_uint(N.FRAME_COUNT, 1 + 8 * step)
+        ctx.ExecuteKernelFrames(k, W * H, 8)
+        mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=dst)
+    ctx.Finish()
+    st = comm.status()
+    assert comm.transport() == (N.COMM_TRANSPORT_COPY_ENGINES_IPC, N.COMM_TRANSPORT_RCCL)
+    assert st["fallback"] and st["fallback_reason"] == "link trial round failed" and st["active"] == "RCCL"
+    assert st["gathers"] == 3 and st["last_xfer_ms"] is not None
+    assert _read(ctx, dst, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+    # the hook off and a new plan: the copy engines again, no fallback
+    comm.set_option(N.COMM_OPT_FAIL_LINKS, 0)
+    comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES_IPC)
+    k.set_uint(N.FRAME_COUNT, 25)
+    ctx.ExecuteKernelFrames(k, W * H, 8)
+    mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=dst)
+    ctx.Finish()
+    st = comm.status()
+    assert not st["fallback"] and st["active"] == "copy engines (IPC links)"
+    assert st["bytes_per_gather"] == W * H * 16 and st["copies_per_gather"] == 1
+    assert _read(ctx, dst, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+    comm.destroy()
+    for b in bufs + [out, dst]:
+        b.release()
+    k.release()
+    ctx.release()
+
+
+@pytest.mark.gpu
+def test_gather_destination_is_part_of_the_plan(cornell):
+    """One rank per process (IPC links): the root cannot tell the other ranks about a new
+    destination, so it refuses one until the plan is rebuilt; a destination released meanwhile
+    stays allocated for the plan (the others' copies may still land in it)."""
+    import clrt
+    W, H = 320, 200
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES_IPC)
+    bufs, out, k = _setup(ctx, cornell, W, H)
+    comm.shard(k)
+    d1 = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    d2 = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    k.set_uint(N.FRAME_COUNT, 1)
+    ctx.ExecuteKernelFrames(k, W * H, 8)
+    mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=d1)
+    with pytest.raises(clrt.RTError) as e:
+        mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=d2)
+    assert e.value.code == -59
+    d1.release()  # pinned by the plan: released when the plan lets go
+    comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES_IPC)  # collective re-plan
+    mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=d2)
+    assert _read(ctx, d2, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+    comm.destroy()
+    for b in bufs + [out, d2]:
+        b.release()
+    k.release()
     ctx.release()
 
 
@@ -222,6 +332,31 @@ def test_bench_rccl_flow_world_of_one(tmp_path, transport):
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "byte-identical" in p.stdout
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    want = {"copy": "copy engines", "rccl": "RCCL", "copy-ipc": "copy engines (IPC links)"}[transport]
+    assert line["n_gpus"] == 1 and line["comm"]["nranks"] == 1
+    assert line["comm"]["effective"] == want and not line["comm"]["fallback"]
+    assert want in line["config"]["parallelism"]
+    (r0,) = line["comm"]["per_rank"]
+    assert r0["render_ms"] > 0 and r0["last_gather_ms"] is not None
+
+
+@pytest.mark.gpu
+def test_bench_line_reports_a_fallback(tmp_path):
+    """The driver's N > 1 line says which transport actually ran: a world whose copy-engine links
+    fail (the test hook) runs -- and is labelled -- RCCL, with the reason, byte-identical."""
+    env = dict(os.environ, RT_COMM_ID_FILE=str(tmp_path / "comm.id"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--force-dist", "--check-gather",
+                        "--transport", "copy-ipc", "--fail-links",
+                        "--width", "1280", "--height", "720", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["comm"]["fallback"] and line["comm"]["effective"] == "RCCL"
+    assert line["comm"]["per_rank"][0]["fallback"] == "link trial round failed"
+    assert "over RCCL" in line["config"]["parallelism"] and "byte-identical" in line["check_gather"]
 
 
 # ---- N > 1 on one GPU: the loopback world (rtCommInitLoopback) ----------------------------------

@@ -92,7 +92,7 @@ def test_short_batches_and_the_global_scene_path(cornell):
 
 def test_pending_frames_survive_releases(cornell):
     """frames still coalescing when the kernel or the context is released are launched first"""
-    r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED)
+    r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, perframe_batch=None)
     for f in (1, 2, 3):
         r.frame(f)
     r.k.release()  # launches frames 1-3, then releases
@@ -106,8 +106,32 @@ def test_pending_frames_survive_releases(cornell):
     r.ctx.release()
 
 
+@pytest.mark.parametrize("expose", ["stream", "pointer"])
+def test_no_coalescing_once_the_host_can_synchronise_outside_the_library(cornell, expose):
+    """A host holding the context's stream or a buffer's device pointer may synchronise with
+    hipStreamSynchronize and read the bytes directly: every frame it enqueued must have launched
+    (the library default batch of 8 is in force)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipDeviceSynchronize.argtypes = []
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, perframe_batch=None)
+    assert r.k.get_tuning("perframe_batch") == 8
+    s = r.ctx.stream() if expose == "stream" else None
+    ptr = r.out.device_pointer()
+    for f in (1, 2, 3):
+        r.frame(f)
+    assert (hip.hipStreamSynchronize(ctypes.c_void_p(s)) if s else hip.hipDeviceSynchronize()) == 0
+    got = np.zeros((r.n, 4), np.float32)
+    assert hip.hipMemcpy(got.ctypes.data, ctypes.c_void_p(ptr), r.n * 16, 2) == 0  # hipMemcpyDeviceToHost
+    want = _run(cornell, 1, [("frame", f) for f in (1, 2, 3)])[1]
+    assert got.tobytes() == want.tobytes()
+    r.close()
+
+
 def test_batch_tuning_range(cornell):
-    r = HipRenderer(cornell, 64, 64)
+    r = HipRenderer(cornell, 64, 64, perframe_batch=None)
     assert r.k.get_tuning("perframe_batch") == 8
     for bad in (0, 9):
         with pytest.raises(Exception):

@@ -21,13 +21,11 @@ from ref_compare import face_ids, load_golden, map_faces, rel_err
 RAD_TOL = 1e-4
 
 
-@pytest.mark.parametrize("variant", ["strict", "shipped"])
-@pytest.mark.parametrize("W,H", [(128, 72), (512, 512)])
+# the committed hit fixtures (the 512x512 one was recorded for the strict build only; its hit count
+# is the SURVEY probe's, test_reference_fixtures_are_consistent)
+@pytest.mark.parametrize("variant,W,H", [("strict", 128, 72), ("shipped", 128, 72), ("strict", 512, 512)])
 def test_oracle_primary_hits_vs_reference(cornell, oracle_mod, variant, W, H):
-    try:
-        g = load_golden(f"ref_{variant}_hits_{W}x{H}")
-    except FileNotFoundError:
-        pytest.skip("fixture not committed for this size/variant")
+    g = load_golden(f"ref_{variant}_hits_{W}x{H}")
     _, ids, t, _ = oracle_mod.render(cornell, W, H, frame_count=1, light_bounces=1, want_hits=True)
     assert int((ids >= 0).sum()) == int((g["ids"] >= 0).sum())      # same hit/miss pixels
     assert np.array_equal(ids >= 0, g["ids"] >= 0)
