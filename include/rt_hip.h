@@ -372,8 +372,10 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out);
 int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out);
 /* A world of processes on one node WITHOUT RCCL -- e.g. several ranks sharing one GPU, which RCCL
  * refuses: rank `rank` of `nranks`, one process each, meeting through files in the directory `dir`
- * (the same for every rank, empty, on a file system they share -- a directory that already holds
- * exchange files is refused, RT_INVALID_VALUE; the caller removes it after rtCommDestroy).  Setup
+ * (the same for every rank, empty, on a file system they share; rank 0 writes the world's id into
+ * it -- a directory holding an earlier world's is refused, RT_INVALID_VALUE -- and the others wait
+ * up to a minute for it, so exchange files an earlier world left are never read; the caller
+ * removes the directory after rtCommDestroy).  Setup
  * exchanges, rtCommAllReduceF64 and rtCommBarrier go through the files (each waits at most a
  * minute for the slowest rank); the gathers run on the copy engines over IPC mappings exactly as
  * in an RCCL world (RT_COMM_TRANSPORT_RCCL is refused).  It ships because it is the only way to

@@ -40,7 +40,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
-#include <dirent.h>
+#include <cerrno>
+#include <unistd.h>
 #include <string>
 #include <thread>
 #include <new>
@@ -170,9 +171,56 @@ struct rt_comm_s {
     // through files in `fdir` (exchange number fseq), the gathers over the copy engines
     std::string fdir;
     uint64_t fseq = 0;
+    uint64_t fnonce = 0;  // the world's id (rank 0's, from fdir/world): part of every exchange file name
 };
 
 namespace {
+
+// a shared world's exchange file: x<world>_<exchange>_r<rank>
+std::string xname(const rt_comm c, uint64_t seq, int q) {
+    char w[17];
+    std::snprintf(w, sizeof(w), "%016llx", (unsigned long long)c->fnonce);
+    return c->fdir + "/x" + w + "_" + std::to_string(seq) + "_r" + std::to_string(q);
+}
+
+// A shared world's id.  Rank 0 publishes it in fdir/world (written aside, then linked into place:
+// a directory that already holds one -- an earlier world's -- is refused); the other ranks wait up
+// to a minute for it.  Exchange files carry it, so files an earlier world left are never read.
+int shared_world_id(rt_comm c) {
+    const std::string path = c->fdir + "/world";
+    if (c->rank == 0) {
+        uint64_t id = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull ^
+                      (uint64_t)getpid() << 32;
+        if (id == 0) id = 1;
+        const std::string tmp = path + ".tmp" + std::to_string(getpid());
+        std::FILE* f = std::fopen(tmp.c_str(), "wb");
+        if (!f) return RT_FILE_NOT_FOUND;
+        const bool ok = std::fwrite(&id, sizeof(id), 1, f) == 1;
+        if (std::fclose(f) != 0 || !ok) {
+            (void)std::remove(tmp.c_str());
+            return RT_OUT_OF_RESOURCES;
+        }
+        const int linked = link(tmp.c_str(), path.c_str());
+        (void)std::remove(tmp.c_str());
+        if (linked != 0) return errno == EEXIST ? RT_INVALID_VALUE : RT_OUT_OF_RESOURCES;
+        c->fnonce = id;
+        return RT_SUCCESS;
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+    for (;;) {
+        if (std::FILE* f = std::fopen(path.c_str(), "rb")) {
+            uint64_t id = 0;
+            const bool ok = std::fread(&id, sizeof(id), 1, f) == 1;
+            std::fclose(f);
+            if (ok && id != 0) {
+                c->fnonce = id;
+                return RT_SUCCESS;
+            }
+        }
+        if (std::chrono::steady_clock::now() > deadline) return RT_OUT_OF_RESOURCES;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+}
 
 // The communicator's transfer and unpack streams run at the device's greatest stream priority.
 // Two reasons, both read off a kernel trace of the world-1 flow (profiles/r04/dist_flow_ab.txt):
@@ -311,7 +359,7 @@ void release(rt_comm c) {
     // of exchange k only after reading all files of exchange k - 1, so those have all been read;
     // the last one may still be awaited by a slower rank (the caller removes the directory)
     for (uint64_t q = 1; !c->fdir.empty() && q < c->fseq; ++q)
-        (void)std::remove((c->fdir + "/x" + std::to_string(q) + "_r" + std::to_string(c->rank)).c_str());
+        (void)std::remove(xname(c, q, c->rank).c_str());
     delete c;
 }
 
@@ -409,7 +457,7 @@ int link_direct(const rt_comm* comms, int n_local, int root) {
 // and reads everyone's, waiting up to a minute for the slowest rank.
 int file_allgather(rt_comm c, const void* mine, size_t n, void* all) {
     const uint64_t seq = ++c->fseq;
-    auto name = [&](int q) { return c->fdir + "/x" + std::to_string(seq) + "_r" + std::to_string(q); };
+    auto name = [&](int q) { return xname(c, seq, q); };
     {
         const std::string tmp = name(c->rank) + ".tmp";
         std::FILE* f = std::fopen(tmp.c_str(), "wb");
@@ -750,16 +798,6 @@ int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_c
     *out = nullptr;
     if (!ctx) return RT_INVALID_CONTEXT;
     if (!dir || !*dir || nranks < 1 || rank < 0 || rank >= nranks) return RT_INVALID_VALUE;
-    // exchange files left by an earlier world would be read as this one's: refuse the directory
-    if (DIR* d = opendir(dir)) {
-        bool stale = false;
-        while (const dirent* ent = readdir(d))
-            stale |= ent->d_name[0] == 'x' && std::strstr(ent->d_name, "_r") != nullptr;
-        closedir(d);
-        if (stale) return RT_INVALID_VALUE;
-    } else {
-        return RT_FILE_NOT_FOUND;
-    }
     hipError_t he = hipSetDevice(ctx->device);
     if (he != hipSuccess) return map_hip(he);
     rt_comm c = new (std::nothrow) rt_comm_s();
@@ -773,7 +811,12 @@ int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_c
         delete c;
         return RT_OUT_OF_HOST_MEMORY;
     }
-    const int rc = comm_streams(c, false);
+    int rc = shared_world_id(c);
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    rc = comm_streams(c, false);
     if (rc) {
         release(c);
         return rc;
@@ -875,8 +918,9 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
     for (int i = 0; i < n_local; ++i)  // coalesced per-frame launches first: the gather reads their output
         if (comms[i]->ctx->pend_k) (void)rti::flush_frames(comms[i]->ctx);
     // the plans (rebuilt, by every rank alike, when the size, the root or the transport changes).
-    // The root's destination is part of the plan: when every rank is in this call a new one
-    // rebuilds it too; a rank alone in its process cannot tell the others, so its root refuses it
+    // The root's destination is part of a copy-engine plan: linked by address (every rank in this
+    // call) a new one rebuilds it; linked by IPC handles the root cannot tell the other processes,
+    // so it refuses a new destination until a collective re-plan
     const bool whole_world = n_local == comms[0]->nranks;
     bool fresh = false;
     for (int i = 0; i < n_local; ++i) {
@@ -884,7 +928,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         hipError_t e = hipSetDevice(c->ctx->device);
         if (e != hipSuccess) return map_hip(e);
         rt_mem dst = c->rank == root ? (root_dst ? root_dst : outs[i]) : nullptr;
-        if (!whole_world && c->rank == root && c->W == W && c->H == H && c->root == root && c->ce && c->target != dst)
+        if (c->ipc_linked && c->rank == root && c->W == W && c->H == H && c->root == root && c->target != dst)
             return RT_INVALID_OPERATION;
         bool built = false;
         int rc = ensure_plan(c, W, H, root, dst, outs[i], &built);

@@ -59,4 +59,9 @@ def test_shared_world_refuses_rccl_and_bad_arguments(tmp_path):
     comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES)
     mg.Comm.barrier([comm])
     comm.destroy()
+    # the directory now holds that world's id: a new world there is refused (its exchange files
+    # could be read as the new world's)
+    with pytest.raises(Exception) as e:
+        mg.Comm.init_shared(ctx, 1, 0, str(tmp_path))
+    assert e.value.code == -30
     ctx.release()
