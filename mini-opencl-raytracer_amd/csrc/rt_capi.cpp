@@ -1288,8 +1288,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             if (!ea || !eb) return fail(RT_OUT_OF_RESOURCES);
             (void)hipEventRecord(ea, as);
         }
-        // (copy-engine gathers of the previous image read `out` in place: the accumulation that
-        // rewrites it comes after their copies)
+        // (a root's gather copies of the previous image read `out`: the accumulation that rewrites
+        // it comes after them)
         e = rti::out_read_wait(ctx, as);
         if (e != hipSuccess) return fail(map_hip(e));
 #ifndef RT_DIAG_NO_ACCUM  // diagnostic A/B builds only (wrong images): the render without its accumulation
@@ -1462,7 +1462,7 @@ int rtEnqueueCopyBufferRectToPointer(rt_context ctx, rt_mem src, size_t src_offs
         hipError_t e = rti::main_tail_wait(ctx, ctx->astream);
         // ... and after the gathers queued so far (their unpack writes a root's image; nothing
         // else on astream waits for it)
-        if (e == hipSuccess && ctx->gpending) e = hipStreamWaitEvent(ctx->astream, ctx->gtail, 0);
+        if (e == hipSuccess) e = rti::gather_wait(ctx, ctx->astream);
         if (e == hipSuccess)
             e = hipMemcpy2DAsync(dst, dst_pitch, static_cast<uint8_t*>(src->dptr) + src_offset, src_pitch,
                                  width_bytes, rows, hipMemcpyDeviceToDevice, ctx->astream);

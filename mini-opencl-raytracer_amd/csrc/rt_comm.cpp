@@ -7,25 +7,34 @@
 // b % nranks == r into its full-size output buffer (rtKernelSetRowInterleave), at the rows they
 // occupy in the image; the gather moves them to the root.
 //
-// Copy-engine transport (default).  Every band is written by the copy engines (SDMA,
-// hipMemcpyDeviceToDeviceNoCU; over xGMI between GPUs) straight from the rank's `out` into the
-// same rows of the root's destination -- mapped into the rank by IPC handle (one ncclAllGather per
-// plan), or by address for ranks driven by one process.  No staging, no pack or unpack copy, no
-// compute unit anywhere: a persistent render holds every CU slot until it drains, and anything
-// that needs one -- RCCL's transfer kernel, the runtime's 2-D blit copies -- waits behind it
-// (profiles/r04/dist_flow_ab.txt).  Per gather k (seq within the plan):
+// Copy-engine transport (default): nothing in a gather's steady state needs a compute unit.  A
+// persistent render holds every CU slot until it drains, and anything that needs one -- RCCL's
+// transfer kernel, the runtime's 2-D blit copies, and ROCclr's hipStreamWriteValue64 /
+// hipStreamWaitValue64, which run as kernels (__amd_rocclr_streamOps*) -- waits behind it and then
+// crawls beside it (profiles/r04/dist_flow_ab.txt, profiles/r05/flag_probe.txt).  So the bytes AND
+// the flags move on the copy engines (SDMA, hipMemcpyDeviceToDeviceNoCU; over xGMI between GPUs):
 //
-//   sender accumulation stream : [accumulate k] (ready)                  [wait sent] [accumulate k+1]
-//   sender communicator stream :        (wait ready)(wait release k-1) [copies k] [arrive k] (sent)
-//   root unpack-stream         : (root's queue so far) [release k-1]   (wait arrive k from all) (gtail)
-//   render streams             : [render k+1 ..............................................]
+//   rank q accumulation stream : [accumulate k] [pack k -> stage[s] (SDMA, per band)] [accumulate k+1]
+//   rank q comm stream         :     (packed k)(release k-1) [bands -> root image (SDMA)] [arrive k (SDMA)]
+//   root unpack stream         : (root's queue so far) [release k-1 -> every rank (SDMA)]
+//   root, first read of image k: (wait arrive k from every rank)
 //
-// `release k-1` (a flag in each sender's memory, or an event within one process) says the root
-// has enqueued gather k and everything it queued before (reads of image k-1) has run: a rank's
-// copies never change the root's image under a read.  `arrive k` (a flag per rank in the root's
-// memory) says the rank's bands of image k are in place; the root's context joins every arrival
-// before its next read (qs, gtail).  `sent` (the rank's copies done) orders the accumulation that
-// rewrites `out` after the copies that read it (rti::out_read_wait).
+// * The pack copies the rank's bands densely into one of two staging slots right after the
+//   accumulation, on the accumulation stream: the next accumulation never waits for anything
+//   across GPUs.  The transfer writes every band from the slot into the rows it occupies in the
+//   root's destination -- mapped into the rank by IPC handle (one ncclAllGather per plan), or by
+//   address for ranks driven by one process: no receive slot, no unpack.
+// * `release k-1` (a flag in each rank's memory, written by the root's copy engine once everything
+//   its context queued before gather k -- reads of image k-1 -- has run): a rank's copies never
+//   change the root's image under a read.  The rank's wait for it is the one waiting kernel of a
+//   gather, and it gates only the transfer.
+// * `arrive k` (a flag per rank in the root's memory, written by the rank's copy engine after its
+//   bands): the root joins the arrivals only when it next reads (rti::join_gather, from qs): no
+//   kernel spins on the root while nobody looks at the image.
+// * The root gathering into another buffer copies its own bands straight from its output (local
+//   copies, ordered by events); gathering into its output, they are in place.
+// * Flag values are copied from a device array holding 0, 1, 2, ... (vals); a plan is rebuilt
+//   before the gather count reaches its end (every rank at the same gather).
 //
 // RCCL transport (RT_COMM_TRANSPORT_RCCL, and the fallback of a world whose copy-engine links do
 // not hold): each rank packs its bands densely into a staging slot on its accumulation stream,
@@ -59,6 +68,7 @@ namespace {
 constexpr unsigned kBandRows = 8;     // = the 8x8 tile height of the persistent schedules
 constexpr size_t kPixelBytes = 16;    // one float3 slot of the output buffer
 constexpr size_t kProbeBytes = 4096;  // per rank, the trial round's copy
+constexpr uint64_t kFlagValues = 1ull << 22;  // flag values 0 .. kFlagValues - 1 (32 MB per rank)
 
 int map_nccl(ncclResult_t r) {
     switch (r) {
@@ -124,7 +134,7 @@ struct rt_comm_s {
     bool reserved = false;      // holds a CU reservation on ctx (rti::reserve_cus)
     int rank = 0, nranks = 1;
     hipStream_t cstream = nullptr;  // transfers (copy engines or RCCL), RCCL setup and reductions
-    hipStream_t ustream = nullptr;  // root: release / arrival waits (copy engines), unpack (RCCL)
+    hipStream_t ustream = nullptr;  // root: releases (copy engines), unpack (RCCL)
     // the plan: one (width, height, root, destination); rebuilt when any changes
     unsigned W = 0, H = 0;
     int root = -1;
@@ -139,17 +149,19 @@ struct rt_comm_s {
     rt_mem target = nullptr;         // root: the plan's destination (pinned)
     uint8_t* peer_target = nullptr;  // the root's destination as this rank addresses it
     std::vector<std::pair<uint64_t, uint64_t>> runs;  // this rank's band runs (image byte offset, bytes)
-    bool sends = false;              // this rank copies its bands (every rank but a root gathering into its out)
-    uint64_t* sflags = nullptr;      // [1] (fine-grained, this rank's memory): images released by the root, seq
+    bool sends = false;              // this rank copies its bands (all but a root gathering into its out)
+    uint64_t* sflags = nullptr;      // [1] (fine-grained, this rank's memory): image released by the root, seq
     uint64_t* rflags = nullptr;      // root, [nranks] (fine-grained): rank q's bands of image seq in place
     uint8_t* probe = nullptr;        // root, [nranks][kProbeBytes] (fine-grained): the trial round's copies
     uint8_t* peer_probe = nullptr;
     uint64_t* peer_rflags = nullptr; // the root's arrival flags, as this rank addresses them
     std::vector<uint64_t*> peer_sflags;  // root: every rank's release flag
     std::vector<void*> ipc_opened;       // IPC mappings to close with the plan
-    hipEvent_t ready = nullptr;      // the bands of `out` are final (accumulation stream)
-    hipEvent_t sent = nullptr;       // this rank's copies of the last gather are done
-    hipEvent_t released = nullptr;   // root, one-process worlds: the previous image is released
+    uint64_t* vals = nullptr;        // device: vals[i] = i, the sources of the flag copies (kFlagValues)
+    uint64_t join_seq = 0;           // root, IPC links: the gather whose arrivals the next read joins
+    hipEvent_t ready = nullptr;      // the root's bands of `out` are final (accumulation stream)
+    hipEvent_t dsent = nullptr;      // the root's own copies (gathering into another buffer) are done
+    hipEvent_t released = nullptr;   // root: the previous image is released (unpack stream)
     hipEvent_t xt0 = nullptr, xt1 = nullptr;  // timing: the last gather's transfer on cstream
     bool xt_valid = false;
     // the copies split over streams of their own, which the runtime spreads over several SDMA
@@ -159,12 +171,12 @@ struct rt_comm_s {
     // (0.790 vs 0.798 ms/frame) and 8 stalled the renders (1.17; profiles/r04/dist_flow_ab.txt)
     hipStream_t xstream[8] = {};
     hipEvent_t xgo = nullptr, xdone[8] = {};
-    // ---- RCCL ----
+    // ---- staging: ranks sending to another rank's root (copy engines); every rank (RCCL) ----
     size_t stage_bytes = 0;
     void* stage[2] = {};                      // this rank's packed bands
-    void* parts[2] = {};                      // root: nranks x stage_bytes received bands
-    hipEvent_t packed[2] = {}, rsent[2] = {}, unpacked[2] = {};
-    bool rsent_valid[2] = {}, unpacked_valid[2] = {};
+    void* parts[2] = {};                      // RCCL root: nranks x stage_bytes received bands
+    hipEvent_t packed[2] = {}, sent[2] = {}, unpacked[2] = {};
+    bool sent_valid[2] = {}, unpacked_valid[2] = {};
     int slot = 0;
     double* scratch = nullptr;  // reductions
     // shared worlds (rtCommInitShared): no RCCL; setup exchanges, reductions and barriers go
@@ -279,29 +291,54 @@ int comm_events(rt_comm c, hipError_t e) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xdone[i], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xgo, hipEventDisableTiming);
-    for (hipEvent_t* ev : {&c->ready, &c->sent, &c->released})
+    for (hipEvent_t* ev : {&c->ready, &c->dsent, &c->released})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&c->xt0);
     if (e == hipSuccess) e = hipEventCreate(&c->xt1);
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
         e = hipEventCreateWithFlags(&c->packed[s], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rsent[s], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sent[s], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->unpacked[s], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64 * sizeof(double));
     return map_hip(e);
 }
 
-// RCCL transport buffers: staging slots on every rank, receive slots on the root
-int rccl_buffers(rt_comm c) {
-    if (c->stage[0]) return RT_SUCCESS;
+// staging slots (a rank sending to another rank's root; every rank of an RCCL plan) and, for an
+// RCCL root, its receive slots
+int stage_buffers(rt_comm c, bool rccl) {
     hipError_t e = hipSuccess;
     for (int s = 0; s < 2 && e == hipSuccess; ++s) {
-        e = hipMalloc(&c->stage[s], std::max<size_t>(c->stage_bytes, 16));
-        if (e == hipSuccess && c->rank == c->root)
+        if (!c->stage[s]) e = hipMalloc(&c->stage[s], std::max<size_t>(c->stage_bytes, 16));
+        if (e == hipSuccess && rccl && c->rank == c->root && !c->parts[s])
             e = hipMalloc(&c->parts[s], std::max<size_t>(c->stage_bytes * c->nranks, 16));
     }
     return map_hip(e);
+}
+int rccl_buffers(rt_comm c) { return stage_buffers(c, true); }
+
+// the flag values' source array, once per communicator
+int flag_values(rt_comm c) {
+    if (c->vals) return RT_SUCCESS;
+    std::vector<uint64_t> v;
+    try {
+        v.resize(kFlagValues);
+    } catch (const std::bad_alloc&) {
+        return RT_OUT_OF_HOST_MEMORY;
+    }
+    for (uint64_t i = 0; i < kFlagValues; ++i) v[i] = i;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->vals), kFlagValues * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMemcpy(c->vals, v.data(), kFlagValues * sizeof(uint64_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess && c->vals) {
+        (void)hipFree(c->vals);
+        c->vals = nullptr;
+    }
+    return map_hip(e);
+}
+
+// a flag word (another device's, or this one's) := v, on the copy engine of stream s
+hipError_t flag_copy(rt_comm c, uint64_t* dst, uint64_t v, hipStream_t s) {
+    return hipMemcpyAsync(dst, c->vals + v, sizeof(uint64_t), hipMemcpyDeviceToDeviceNoCU, s);
 }
 
 void free_buffers(rt_comm c) {
@@ -311,7 +348,7 @@ void free_buffers(rt_comm c) {
         if (c->stage[s]) (void)hipFree(c->stage[s]);
         if (c->parts[s]) (void)hipFree(c->parts[s]);
         c->stage[s] = c->parts[s] = nullptr;
-        c->rsent_valid[s] = c->unpacked_valid[s] = false;
+        c->sent_valid[s] = c->unpacked_valid[s] = false;
     }
     for (uint64_t** f : {&c->sflags, &c->rflags})
         if (*f) (void)hipFree(*f);
@@ -324,12 +361,13 @@ void free_buffers(rt_comm c) {
     c->runs.clear();
     c->ce = c->ipc_linked = c->sends = false;
     c->fallback_reason = RT_COMM_FALLBACK_NONE;
-    c->seq = 0;
+    c->seq = c->join_seq = 0;
     c->xt_valid = false;
     c->slot = 0;
     c->W = c->H = 0;
     c->root = -1;
-    if (c->ctx->oread_ev == c->sent) c->ctx->oread = false;
+    if (c->ctx->oread_ev == c->dsent) c->ctx->oread = false;
+    if (c->ctx->gjoin == c) c->ctx->gjoin = nullptr;
 }
 
 void release(rt_comm c) {
@@ -339,16 +377,17 @@ void release(rt_comm c) {
     for (hipStream_t s : c->xstream)
         if (s) (void)hipStreamSynchronize(s);
     free_buffers(c);
-    if (c->ctx->oread_ev == c->sent) c->ctx->oread_ev = nullptr;
+    if (c->ctx->oread_ev == c->dsent) c->ctx->oread_ev = nullptr;
     for (int s = 0; s < 2; ++s)
-        for (hipEvent_t ev : {c->packed[s], c->rsent[s], c->unpacked[s]})
+        for (hipEvent_t ev : {c->packed[s], c->sent[s], c->unpacked[s]})
             if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : {c->ready, c->sent, c->released, c->xt0, c->xt1, c->xgo})
+    for (hipEvent_t ev : {c->ready, c->dsent, c->released, c->xt0, c->xt1, c->xgo})
         if (ev) (void)hipEventDestroy(ev);
     for (int i = 0; i < 8; ++i) {
         if (c->xstream[i]) (void)hipStreamDestroy(c->xstream[i]);
         if (c->xdone[i]) (void)hipEventDestroy(c->xdone[i]);
     }
+    if (c->vals) (void)hipFree(c->vals);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
@@ -375,10 +414,12 @@ void quiesce(rt_comm c) {
 // The plan of a W x H gather into `dst` (the root's destination; ranks other than the root pass
 // nullptr) from `out` -- all earlier gathers of this comm have completed when it is rebuilt.  A
 // copy-engine plan writes into the destination it was linked to, so a new one rebuilds it (the
-// RCCL transport unpacks into whatever the call names).
+// RCCL transport unpacks into whatever the call names); so does a gather count about to run past
+// the flag values (every rank of the world at the same gather).
 int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, rt_mem dst, rt_mem out, bool* built) {
     *built = false;
-    if (c->W == W && c->H == H && c->root == root && (c->rank != root || !c->ce || dst == c->target))
+    if (c->W == W && c->H == H && c->root == root && (c->rank != root || !c->ce || dst == c->target) &&
+        c->seq + 2 < kFlagValues)
         return RT_SUCCESS;
     *built = true;
     quiesce(c);
@@ -403,10 +444,14 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, rt_mem dst, rt_mem 
     // the root gathering into its own output has its bands in place already
     c->sends = c->rank != root || dst != out;
     if (c->transport == RT_COMM_TRANSPORT_RCCL) return rccl_buffers(c);
-    // copy engines: every flag word and the probe are fine-grained memory (written by other
-    // devices' engines, read coherently by the waits and the host), each its own allocation (an
-    // IPC handle maps a whole allocation)
+    // copy engines: the release and arrival flags and the probe are fine-grained memory (written
+    // by other devices' engines, read coherently by the waits and the host), each its own
+    // allocation (an IPC handle maps a whole allocation)
     c->runs = band_runs(c->plans[c->rank]);
+    if (c->rank != root) {
+        const int rc = stage_buffers(c, false);
+        if (rc) return rc;
+    }
     hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sflags), sizeof(uint64_t), hipDeviceMallocFinegrained);
     if (e == hipSuccess && c->rank == root)
         e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->rflags), sizeof(uint64_t) * c->nranks,
@@ -420,8 +465,8 @@ int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, rt_mem dst, rt_mem 
 }
 
 // Copy-engine links of a plan whose members are all in this call (loopback worlds, and RCCL
-// worlds driven by one process): the root's destination by address.  Between devices the copy
-// engines reach peer memory once peer access is on.
+// worlds driven by one process): the root's destination by address, the steps ordered by events.
+// Between devices the copy engines reach peer memory once peer access is on.
 int link_direct(const rt_comm* comms, int n_local, int root) {
     rt_comm R = nullptr;
     for (int i = 0; i < n_local; ++i)
@@ -530,13 +575,13 @@ bool poll_words(const uint64_t* dev, size_t n, uint64_t v, std::chrono::steady_c
     }
 }
 
-// One trial round over fresh IPC links: every rank copies a 4-KB pattern into its part of the
-// root's probe on the copy engines and raises its arrival flag; the root waits for every flag
-// (from the host, then -- once they are in memory -- with the stream waits gathers use), checks
-// every pattern, raises every rank's release flag; each rank waits for its own the same two
-// ways; all flags go back to 0.  Returns 1 when anything failed or timed out.
+// One trial round over fresh IPC links, with the production signalling: every rank copies a 4-KB
+// pattern into its part of the root's probe and its arrival flag := 1 (copy engines); the root
+// waits for every flag (from the host, then -- once they are in memory -- with the stream waits a
+// read of the image uses), checks every pattern, copies release := 1 into every rank's flag; each
+// rank waits for its own the same two ways; all flags go back to 0.  Returns 1 when anything
+// failed or timed out.
 int ipc_handshake(rt_comm c) {
-    constexpr uint64_t kMagic = 0x52545f4c494e4b31ull;
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(20);
     uint8_t* src = nullptr;
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&src), kProbeBytes);
@@ -544,15 +589,14 @@ int ipc_handshake(rt_comm c) {
     if (e == hipSuccess)
         e = hipMemcpyAsync(c->peer_probe + (size_t)c->rank * kProbeBytes, src, kProbeBytes,
                            hipMemcpyDeviceToDeviceNoCU, c->cstream);
-    if (e == hipSuccess) e = hipStreamWriteValue64(c->cstream, c->peer_rflags + c->rank, kMagic, 0);
+    if (e == hipSuccess) e = flag_copy(c, c->peer_rflags + c->rank, 1, c->cstream);
     const bool sent_ok = e == hipSuccess && wait_until(c->cstream, deadline);
     if (src) (void)hipFree(src);
     if (!sent_ok) return 1;
     if (c->rank == c->root) {
-        if (!poll_words(c->rflags, (size_t)c->nranks, kMagic, deadline)) return 1;
-        // the flags are in memory; the root stream's waits must see them too (the production path)
+        if (!poll_words(c->rflags, (size_t)c->nranks, 1, deadline)) return 1;
         for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-            e = hipStreamWaitValue64(c->ustream, c->rflags + q, kMagic, hipStreamWaitValueGte, ~0ull);
+            e = hipStreamWaitValue64(c->ustream, c->rflags + q, 1, hipStreamWaitValueGte, ~0ull);
         if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
         std::vector<uint8_t> got(kProbeBytes);
         for (int q = 0; q < c->nranks; ++q) {
@@ -561,13 +605,12 @@ int ipc_handshake(rt_comm c) {
             for (uint8_t b : got)
                 if (b != (uint8_t)((q + 1) & 0xff)) return 1;
         }
-        for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
-            e = hipStreamWriteValue64(c->ustream, c->peer_sflags[q], kMagic, 0);
+        for (int q = 0; q < c->nranks && e == hipSuccess; ++q) e = flag_copy(c, c->peer_sflags[q], 1, c->ustream);
         if (e == hipSuccess) e = hipMemsetAsync(c->rflags, 0, sizeof(uint64_t) * c->nranks, c->ustream);
         if (e != hipSuccess || !wait_until(c->ustream, deadline)) return 1;
     }
-    if (!poll_words(c->sflags, 1, kMagic, deadline)) return 1;
-    e = hipStreamWaitValue64(c->cstream, c->sflags, kMagic, hipStreamWaitValueGte, ~0ull);
+    if (!poll_words(c->sflags, 1, 1, deadline)) return 1;
+    e = hipStreamWaitValue64(c->cstream, c->sflags, 1, hipStreamWaitValueGte, ~0ull);
     if (e != hipSuccess || !wait_until(c->cstream, deadline)) return 1;
     e = hipMemset(c->sflags, 0, sizeof(uint64_t));
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -579,6 +622,7 @@ int link_ipc(rt_comm c) {
     IpcBlob mine{};
     // 0: links hold; RT_COMM_FALLBACK_IPC_MAP / _HANDSHAKE: why not (the world agrees on the max)
     int bad = c->fail_links ? RT_COMM_FALLBACK_HANDSHAKE : 0;
+    if (e == hipSuccess && flag_values(c) != RT_SUCCESS) bad = RT_COMM_FALLBACK_HANDSHAKE;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.sflags, c->sflags);
     if (e == hipSuccess && c->rank == c->root) {
         e = hipIpcGetMemHandle(&mine.target, c->target->dptr);
@@ -875,7 +919,9 @@ int rtCommGetStatus(rt_comm c, rt_comm_status* out) {
     if (c->W != 0 && c->ce) {
         if (c->sends)
             for (const auto& r : c->runs) out->bytes_per_gather += r.second;
-        out->copies_per_gather = c->sends ? (unsigned)c->runs.size() : 0u;
+        // the root: its own bands straight into the destination; the others: pack + transfer + flag
+        const unsigned n = (unsigned)c->runs.size();
+        out->copies_per_gather = !c->sends ? 0u : c->rank == c->root ? n : 2u * n + (c->ipc_linked ? 1u : 0u);
     } else if (c->W != 0) {
         out->bytes_per_gather = c->stage_bytes;
         out->copies_per_gather = 1;
@@ -974,7 +1020,7 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         // the bands are final after every accumulation enqueued so far (astream, in order) and
         // after whatever the main stream has queued (per-frame launches write `out` there)
         e = rti::main_tail_wait(ctx, ctx->astream);
-        if (e == hipSuccess && c->rsent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->rsent[s], 0);  // slot free
+        if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);  // slot free
         if (e == hipSuccess)
             e = copy_rects(c->plans[c->rank], out, static_cast<uint8_t*>(c->stage[s]), true, ctx->astream);
         if (e == hipSuccess) e = hipEventRecord(c->packed[s], ctx->astream);
@@ -1016,59 +1062,66 @@ int rccl_transfer(const rt_comm* comms, int n_local, int root) {
     return rc_end;
 }
 
-// The rank's band runs on the copy engines, after and before everything on the communicator
-// stream: the bytes dealt out over the transfer streams in image order, in pieces of at least
-// 1 MiB (several ranks driven by one process share its hardware queues, so they copy on the one
-// stream).  The destination is the root's image (or, for a root gathering into another buffer,
-// that buffer) at the same offsets.
-hipError_t copy_bands(rt_comm c, const uint8_t* src) {
+// Copies of this rank's band runs on the copy engines: run i (image offset o_i, n_i bytes, dense
+// offset d_i -- its place in the staging slot) from src + (src_dense ? d_i : o_i) to
+// dst + (dst_dense ? d_i : o_i).  On stream `s` alone, or (split) dealt out over the transfer
+// streams in image order in pieces of at least 1 MiB, after and before everything on `s`.
+hipError_t copy_runs(rt_comm c, hipStream_t s, bool split, uint8_t* dst, bool dst_dense, const uint8_t* src,
+                     bool src_dense) {
     uint64_t total = 0;
     for (const auto& r : c->runs) total += r.second;
-    const bool shared = !c->ipc_linked && c->nranks > 1;
-    const size_t k = shared ? 1 : std::max<size_t>(1, std::min<uint64_t>(RT_COMM_XFER_STREAMS, total >> 20));
-    auto copy = [&](uint64_t off, uint64_t n, hipStream_t s) {
-        return hipMemcpyAsync(c->peer_target + off, src + off, n, hipMemcpyDeviceToDeviceNoCU, s);
+    const size_t k = split ? std::max<size_t>(1, std::min<uint64_t>(RT_COMM_XFER_STREAMS, total >> 20)) : 1;
+    auto copy = [&](size_t run, uint64_t dense, uint64_t at, uint64_t n, hipStream_t st) {
+        const uint64_t o = c->runs[run].first + at, d = dense + at;
+        return hipMemcpyAsync(dst + (dst_dense ? d : o), src + (src_dense ? d : o), n, hipMemcpyDeviceToDeviceNoCU, st);
     };
     if (k == 1) {
-        for (const auto& r : c->runs)
-            if (hipError_t e = copy(r.first, r.second, c->cstream)) return e;
+        uint64_t dense = 0;
+        for (size_t i = 0; i < c->runs.size(); ++i) {
+            if (hipError_t e = copy(i, dense, 0, c->runs[i].second, s)) return e;
+            dense += c->runs[i].second;
+        }
         return hipSuccess;
     }
-    hipError_t e = hipEventRecord(c->xgo, c->cstream);
+    hipError_t e = hipEventRecord(c->xgo, s);
     const uint64_t share = ((total + k - 1) / k + 255) & ~(uint64_t)255;
     size_t run = 0;
-    uint64_t run_done = 0;  // bytes of runs[run] already dealt out
+    uint64_t run_done = 0, dense = 0;  // bytes of runs[run] already dealt out; its dense offset
     for (size_t i = 0; i < k && e == hipSuccess && run < c->runs.size(); ++i) {
         e = hipStreamWaitEvent(c->xstream[i], c->xgo, 0);
         uint64_t left = share;
         while (e == hipSuccess && left > 0 && run < c->runs.size()) {
-            const auto& r = c->runs[run];
-            const uint64_t n = std::min(left, r.second - run_done);
-            e = copy(r.first + run_done, n, c->xstream[i]);
+            const uint64_t n = std::min(left, c->runs[run].second - run_done);
+            e = copy(run, dense, run_done, n, c->xstream[i]);
             left -= n;
             run_done += n;
-            if (run_done == r.second) {
+            if (run_done == c->runs[run].second) {
+                dense += run_done;
                 ++run;
                 run_done = 0;
             }
         }
         if (e == hipSuccess) e = hipEventRecord(c->xdone[i], c->xstream[i]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->xdone[i], 0);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, c->xdone[i], 0);
     }
     return e;
 }
 
-// Copy-engine gather (see the top of the file).  Between processes (IPC links), flags carry the
-// gather's sequence number seq (1, 2, ... within a plan): rflags[q] = seq when rank q's bands of
-// image seq are in the root's destination, sflags = seq when the root has released image seq (its
-// reads of it are done) -- a rank's copies of image seq + 1 wait for it.  Ranks driven by this
-// process (loopback worlds, rtCommInitAll) order the same steps with events instead (the root's
-// `released`, the senders' `sent`): no waiting packet on a hardware queue their other streams
-// share.
+// Copy-engine gather (see the top of the file).  Flags carry the gather's sequence number seq
+// (1, 2, ... within a plan): rflags[q] = seq when rank q's bands of image seq are in the root's
+// destination, sflags = seq when the root has released image seq (everything its context queued
+// before gather seq + 1 has run) -- a rank's transfer of image seq + 1 waits for it.  Ranks driven
+// by this process (loopback worlds, rtCommInitAll) order the same steps with events instead (the
+// root's `released`, the ranks' `sent`), joined by the root at once (events wait without a
+// kernel).
 int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
     rt_comm R = nullptr;  // the root, when it is driven by this call
+    rt_mem Rout = nullptr;
     for (int i = 0; i < n_local; ++i)
-        if (comms[i]->rank == root) R = comms[i];
+        if (comms[i]->rank == root) {
+            R = comms[i];
+            Rout = outs[i];
+        }
     // 1. the root releases the previous image once everything its context queued so far has run
     if (R) {
         hipError_t e = hipSetDevice(R->ctx->device);
@@ -1077,55 +1130,91 @@ int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
         // (reads on the accumulation stream: rtContextSetReadbackOnAccumStream)
         if (e == hipSuccess && R->ctx->readback_on_astream) e = hipStreamWaitEvent(R->ustream, R->ctx->atail, 0);
         for (int q = 0; R->ipc_linked && prev > 0 && q < R->nranks && e == hipSuccess; ++q)
-            if (q != root || R->sends) e = hipStreamWriteValue64(R->ustream, R->peer_sflags[q], prev, 0);
-        if (e == hipSuccess && !R->ipc_linked) e = hipEventRecord(R->released, R->ustream);
-        if (e != hipSuccess) return map_hip(e);
-    }
-    // 2. every sending rank copies its bands of `out` into the root's destination
-    for (int i = 0; i < n_local; ++i) {
-        rt_comm c = comms[i];
-        rt_context ctx = c->ctx;
-        const uint64_t seq = ++c->seq;
-        hipError_t e = hipSetDevice(ctx->device);
-        if (e == hipSuccess && c->sends) {
-            // the bands are final after the accumulations (astream) and the per-frame launches
-            // (main stream) queued so far
+            if (q != root) e = flag_copy(R, R->peer_sflags[q], prev, R->ustream);
+        if (e == hipSuccess) e = hipEventRecord(R->released, R->ustream);
+        // 1b. gathering into another buffer, the root copies its own bands there straight from its
+        // output: after the accumulations and per-frame launches that wrote them, after the reads
+        // of the previous image; the next accumulation waits for the copies (out_read_wait)
+        if (e == hipSuccess && R->sends) {
+            rt_context ctx = R->ctx;
+            ++R->seq;
             e = rti::main_tail_wait(ctx, ctx->astream);
-            if (e == hipSuccess) e = hipEventRecord(c->ready, ctx->astream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->ready, 0);
-            if (e == hipSuccess && seq > 1) {  // the root is done with the previous image
-                e = c->ipc_linked ? hipStreamWaitValue64(c->cstream, c->sflags, seq - 1, hipStreamWaitValueGte, ~0ull)
-                                  : hipStreamWaitEvent(c->cstream, R->released, 0);
-            }
-            if (e == hipSuccess) e = hipEventRecord(c->xt0, c->cstream);
-            if (e == hipSuccess) e = copy_bands(c, static_cast<const uint8_t*>(outs[i]->dptr));
-            if (e == hipSuccess) e = hipEventRecord(c->xt1, c->cstream);
-            if (e == hipSuccess && c->ipc_linked)
-                e = hipStreamWriteValue64(c->cstream, c->peer_rflags + c->rank, seq, 0);
-            if (e == hipSuccess) e = hipEventRecord(c->sent, c->cstream);
+            if (e == hipSuccess) e = hipEventRecord(R->ready, ctx->astream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(R->cstream, R->ready, 0);
+            if (e == hipSuccess) e = hipStreamWaitEvent(R->cstream, R->released, 0);
+            if (e == hipSuccess) e = hipEventRecord(R->xt0, R->cstream);
+            if (e == hipSuccess)
+                e = copy_runs(R, R->cstream, true, static_cast<uint8_t*>(R->target->dptr), false,
+                              static_cast<const uint8_t*>(Rout->dptr), false);
+            if (e == hipSuccess) e = hipEventRecord(R->xt1, R->cstream);
+            if (e == hipSuccess) e = hipEventRecord(R->dsent, R->cstream);
             if (e == hipSuccess) {
-                c->xt_valid = true;
-                // the accumulation that next rewrites `out` waits for these copies
-                ctx->oread_ev = c->sent;
+                R->xt_valid = true;
+                ctx->oread_ev = R->dsent;
                 ctx->oread = true;
             }
+        } else if (e == hipSuccess) {
+            ++R->seq;
         }
-        // reads on a sender's context wait for its copies (qs)
-        if (e == hipSuccess && c != R) e = hipEventRecord(ctx->gtail, c->cstream);
         if (e != hipSuccess) return map_hip(e);
-        if (c != R) ctx->gpending = true;
     }
-    // 3. the root's context joins every rank's arrival
+    // 2. every other rank: pack its bands into a staging slot right after the accumulation
+    // (accumulation stream: the next accumulation never waits across GPUs), then -- once the root
+    // has released the previous image -- transfer them into the root's destination and raise its
+    // arrival flag, all on the copy engines
+    for (int i = 0; i < n_local; ++i) {
+        rt_comm c = comms[i];
+        if (c == R) continue;
+        rt_context ctx = c->ctx;
+        const uint64_t seq = ++c->seq;
+        const int s = c->slot;
+        hipError_t e = hipSetDevice(ctx->device);
+        if (e == hipSuccess) e = rti::main_tail_wait(ctx, ctx->astream);
+        if (e == hipSuccess && c->sent_valid[s]) e = hipStreamWaitEvent(ctx->astream, c->sent[s], 0);  // slot free
+        if (e == hipSuccess)
+            e = copy_runs(c, ctx->astream, false, static_cast<uint8_t*>(c->stage[s]), true,
+                          static_cast<const uint8_t*>(outs[i]->dptr), false);
+        if (e == hipSuccess) e = hipEventRecord(c->packed[s], ctx->astream);
+        if (e == hipSuccess) e = hipEventRecord(ctx->atail, ctx->astream);
+        if (e == hipSuccess) ctx->apending = true;
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->cstream, c->packed[s], 0);
+        if (e == hipSuccess && seq > 1) {  // the root is done with the previous image
+            e = c->ipc_linked ? hipStreamWaitValue64(c->cstream, c->sflags, seq - 1, hipStreamWaitValueGte, ~0ull)
+                              : hipStreamWaitEvent(c->cstream, R->released, 0);
+        }
+        if (e == hipSuccess) e = hipEventRecord(c->xt0, c->cstream);
+        if (e == hipSuccess)
+            e = copy_runs(c, c->cstream, !(!c->ipc_linked && c->nranks > 1), c->peer_target, false,
+                          static_cast<const uint8_t*>(c->stage[s]), true);
+        if (e == hipSuccess) e = hipEventRecord(c->xt1, c->cstream);
+        if (e == hipSuccess && c->ipc_linked) e = flag_copy(c, c->peer_rflags + c->rank, seq, c->cstream);
+        if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
+        // reads on this rank's context wait for its transfer (qs)
+        if (e == hipSuccess) e = hipEventRecord(ctx->gtail, c->cstream);
+        if (e != hipSuccess) return map_hip(e);
+        c->sent_valid[s] = true;
+        c->xt_valid = true;
+        ctx->gpending = true;
+        c->slot ^= 1;
+    }
+    // 3. the root's context joins the arrivals: by events at once (one process), or -- between
+    // processes -- with flag waits enqueued only when the image is next read (join_gather)
     if (R) {
         hipError_t e = hipSetDevice(R->ctx->device);
-        const uint64_t seq = R->seq;
-        for (int q = 0; R->ipc_linked && q < R->nranks && e == hipSuccess; ++q)
-            if (q != root || R->sends) e = hipStreamWaitValue64(R->ustream, R->rflags + q, seq, hipStreamWaitValueGte, ~0ull);
-        for (int j = 0; !R->ipc_linked && j < n_local && e == hipSuccess; ++j)
-            if (comms[j]->sends) e = hipStreamWaitEvent(R->ustream, comms[j]->sent, 0);
-        if (e == hipSuccess) e = hipEventRecord(R->ctx->gtail, R->ustream);
-        if (e != hipSuccess) return map_hip(e);
-        R->ctx->gpending = true;
+        if (R->ipc_linked) {
+            R->join_seq = R->seq;
+            R->ctx->gjoin = R;
+            R->ctx->gpending = false;
+        } else {
+            for (int j = 0; j < n_local && e == hipSuccess; ++j) {
+                rt_comm c = comms[j];
+                if (c != R) e = hipStreamWaitEvent(R->ustream, c->sent[c->slot ^ 1], 0);
+            }
+            if (e == hipSuccess && R->sends) e = hipStreamWaitEvent(R->ustream, R->dsent, 0);
+            if (e == hipSuccess) e = hipEventRecord(R->ctx->gtail, R->ustream);
+            if (e != hipSuccess) return map_hip(e);
+            R->ctx->gpending = true;
+        }
     }
     return RT_SUCCESS;
 }
@@ -1138,10 +1227,10 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
         const int s = c->slot;
         hipError_t e = hipSetDevice(ctx->device);
         if (e == hipSuccess) e = hipEventRecord(c->xt1, c->cstream);
-        if (e == hipSuccess) e = hipEventRecord(c->rsent[s], c->cstream);
+        if (e == hipSuccess) e = hipEventRecord(c->sent[s], c->cstream);
         if (e != hipSuccess) return map_hip(e);
         c->xt_valid = true;
-        c->rsent_valid[s] = true;
+        c->sent_valid[s] = true;
         if (c->rank == root) {
             // Gathering into the root's own output: its own bands are in place already and are
             // not unpacked, so the unpack writes only other ranks' rows, which no later render,
@@ -1155,7 +1244,7 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
             const bool into_out = !root_dst || root_dst == outs[i];
             uint8_t* dst = static_cast<uint8_t*>((root_dst ? root_dst : outs[i])->dptr);
             e = rti::main_tail_wait(ctx, c->ustream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(c->ustream, c->rsent[s], 0);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->ustream, c->sent[s], 0);
             for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
                 if (!(into_out && q == c->rank))
                     e = copy_rects(c->plans[q], dst, static_cast<uint8_t*>(c->parts[s]) + (size_t)q * c->stage_bytes,
@@ -1171,6 +1260,21 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
     }
     return RT_SUCCESS;
 }
+
+}  // namespace
+
+// The root's first read of an image gathered between processes: `s` waits for every rank's arrival
+// flag (and the root's own copies), and the context's gather tail becomes that point of `s`.
+hipError_t rti::join_gather(rt_comm c, hipStream_t s) {
+    hipError_t e = hipSetDevice(c->ctx->device);
+    for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+        if (q != c->root) e = hipStreamWaitValue64(s, c->rflags + q, c->join_seq, hipStreamWaitValueGte, ~0ull);
+    if (e == hipSuccess && c->sends) e = hipStreamWaitEvent(s, c->dsent, 0);
+    if (e == hipSuccess) e = hipEventRecord(c->ctx->gtail, s);
+    return e;
+}
+
+namespace {
 
 // a loopback world's calls must name all its members, each once
 int check_loopback(const rt_comm* comms, int n_local) {

@@ -61,8 +61,12 @@ struct rt_context_s {
     // the accumulations, so reads of the gathered image are ordered after it
     hipEvent_t gtail = nullptr;
     bool gpending = false;
-    // copy-engine gathers read the output buffer in place (rt_comm.cpp ce_gather): the next
-    // accumulation -- which rewrites it -- waits for their copies (oread_ev, the comm's `sent`)
+    // a copy-engine gather between processes whose arrivals the root has not joined yet: the
+    // stream that next reads the image waits for the arrival flags (rti::join_gather) -- no
+    // waiting kernel is enqueued while nobody reads (rt_comm.cpp)
+    rt_comm gjoin = nullptr;
+    // a root gathering into another buffer copies its own bands straight from its output: the
+    // next accumulation -- which rewrites the output -- waits for those copies (oread_ev)
     hipEvent_t oread_ev = nullptr;
     bool oread = false;
     // per-frame launches queued back to back and not launched yet (rt_capi.cpp, frame
@@ -109,6 +113,25 @@ inline int map_hip(hipError_t e) {
 // which is also kept in ctx->pend_error for the next call that reports one.
 int flush_frames(rt_context ctx);
 
+// `s` waits for the root's pending gather arrivals (rt_comm.cpp; records gtail behind them)
+hipError_t join_gather(rt_comm c, hipStream_t s);
+
+// `s` waits for the gathers enqueued on the context so far (reads of a gathered image)
+inline hipError_t gather_wait(rt_context ctx, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (ctx->gjoin) {
+        e = join_gather(ctx->gjoin, s);  // (then gtail is the joining stream's tail)
+        ctx->gjoin = nullptr;
+        ctx->gpending = e == hipSuccess && s != ctx->stream;
+        return e;
+    }
+    if (ctx->gpending) {
+        e = hipStreamWaitEvent(s, ctx->gtail, 0);
+        if (s == ctx->stream) ctx->gpending = false;
+    }
+    return e;
+}
+
 // The context's stream, after every pending accumulation and gather (see rt_context_s) and the
 // coalesced per-frame launches.
 inline hipStream_t qs(rt_context ctx) {
@@ -117,10 +140,7 @@ inline hipStream_t qs(rt_context ctx) {
         (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
         ctx->apending = false;
     }
-    if (ctx->gpending) {
-        (void)hipStreamWaitEvent(ctx->stream, ctx->gtail, 0);
-        ctx->gpending = false;
-    }
+    (void)gather_wait(ctx, ctx->stream);
     ctx->mdirty = true;  // the caller enqueues on it
     return ctx->stream;
 }
@@ -140,7 +160,7 @@ inline hipError_t main_tail_wait(rt_context ctx, hipStream_t s) {
     return hipStreamWaitEvent(s, ctx->mtail, 0);
 }
 
-// the next accumulation launch on `s` rewrites the output: after the gathers reading it in place
+// the next accumulation launch on `s` rewrites the output: after the gather copies reading it
 inline hipError_t out_read_wait(rt_context ctx, hipStream_t s) {
     if (!ctx->oread) return hipSuccess;
     ctx->oread = false;
