@@ -53,6 +53,7 @@
 #include <unistd.h>
 #include <string>
 #include <thread>
+#include <memory>
 #include <new>
 #include <utility>
 #include <vector>
@@ -159,6 +160,10 @@ struct rt_comm_s {
     std::vector<void*> ipc_opened;       // IPC mappings to close with the plan
     uint64_t* vals = nullptr;        // device: vals[i] = i, the sources of the flag copies (kFlagValues)
     uint64_t join_seq = 0;           // root, IPC links: the gather whose arrivals the next read joins
+    std::vector<hipEvent_t> join_events;  // root, one process: the ranks' `sent` events of that gather
+    // one-process worlds (rtCommInitLoopback, rtCommInitAll): the members still alive -- a member
+    // released before its root joined takes its events out of the root's join (it has drained)
+    std::shared_ptr<std::vector<rt_comm>> members;
     hipEvent_t ready = nullptr;      // the root's bands of `out` are final (accumulation stream)
     hipEvent_t dsent = nullptr;      // the root's own copies (gathering into another buffer) are done
     hipEvent_t released = nullptr;   // root: the previous image is released (unpack stream)
@@ -376,6 +381,14 @@ void release(rt_comm c) {
         if (s) (void)hipStreamSynchronize(s);
     for (hipStream_t s : c->xstream)
         if (s) (void)hipStreamSynchronize(s);
+    if (c->members) {  // (its transfers have drained: nobody needs to wait for its events)
+        auto& m = *c->members;
+        m.erase(std::remove(m.begin(), m.end(), c), m.end());
+        for (rt_comm o : m)
+            o->join_events.erase(std::remove_if(o->join_events.begin(), o->join_events.end(),
+                                                [&](hipEvent_t ev) { return ev == c->sent[0] || ev == c->sent[1]; }),
+                                 o->join_events.end());
+    }
     free_buffers(c);
     if (c->ctx->oread_ev == c->dsent) c->ctx->oread_ev = nullptr;
     for (int s = 0; s < 2; ++s)
@@ -721,6 +734,15 @@ hipError_t copy_rects(const std::vector<rt_rect>& plan, uint8_t* img, uint8_t* s
 }
 
 int rccl_transfer(const rt_comm* comms, int n_local, int root);
+// the members of a one-process world know each other (rt_comm_s::members)
+void link_members(rt_comm* comms, int n) {
+    try {
+        auto m = std::make_shared<std::vector<rt_comm>>(comms, comms + n);
+        for (int i = 0; i < n; ++i) comms[i]->members = m;
+    } catch (const std::bad_alloc&) {  // (no exception crosses the C ABI; a join then waits at once)
+        for (int i = 0; i < n; ++i) comms[i]->members.reset();
+    }
+}
 int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, const rt_mem* outs);
 int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs);
 int check_loopback(const rt_comm* comms, int n_local);
@@ -801,6 +823,7 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
         }
         comms_out[i] = c;
     }
+    link_members(comms_out, n);
     return RT_SUCCESS;
 }
 
@@ -834,6 +857,7 @@ int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
         }
         comms_out[i] = c;
     }
+    link_members(comms_out, n);
     return RT_SUCCESS;
 }
 
@@ -1197,24 +1221,27 @@ int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
         ctx->gpending = true;
         c->slot ^= 1;
     }
-    // 3. the root's context joins the arrivals: by events at once (one process), or -- between
-    // processes -- with flag waits enqueued only when the image is next read (join_gather)
+    // 3. the root's context joins the arrivals when the image is next read (join_gather): flag
+    // waits between processes, the ranks' events within one.  Nothing waits at gather time: even
+    // an event wait on the root's stream cost the world-1 flow 2 % (0.804 vs 0.788 ms/frame,
+    // profiles/r05/gather_world1_ab.txt)
     if (R) {
-        hipError_t e = hipSetDevice(R->ctx->device);
-        if (R->ipc_linked) {
-            R->join_seq = R->seq;
-            R->ctx->gjoin = R;
-            R->ctx->gpending = false;
-        } else {
-            for (int j = 0; j < n_local && e == hipSuccess; ++j) {
-                rt_comm c = comms[j];
-                if (c != R) e = hipStreamWaitEvent(R->ustream, c->sent[c->slot ^ 1], 0);
-            }
+        R->join_seq = R->seq;
+        R->join_events.clear();
+XX
+            hipError_t e = hipSetDevice(R->ctx->device);
+            for (int j = 0; j < n_local && e == hipSuccess; ++j)
+                if (comms[j] != R) e = hipStreamWaitEvent(R->ustream, comms[j]->sent[comms[j]->slot ^ 1], 0);
             if (e == hipSuccess && R->sends) e = hipStreamWaitEvent(R->ustream, R->dsent, 0);
             if (e == hipSuccess) e = hipEventRecord(R->ctx->gtail, R->ustream);
             if (e != hipSuccess) return map_hip(e);
             R->ctx->gpending = true;
+            return RT_SUCCESS;
         }
+        for (int j = 0; !R->ipc_linked && j < n_local; ++j)
+            if (comms[j] != R) R->join_events.push_back(comms[j]->sent[comms[j]->slot ^ 1]);
+        R->ctx->gjoin = R;
+        R->ctx->gpending = false;
     }
     return RT_SUCCESS;
 }
@@ -1263,12 +1290,14 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
 
 }  // namespace
 
-// The root's first read of an image gathered between processes: `s` waits for every rank's arrival
-// flag (and the root's own copies), and the context's gather tail becomes that point of `s`.
+// The root's first read of a gathered image: `s` waits for every rank's arrival (flags between
+// processes, events within one; and the root's own copies), and the context's gather tail
+// becomes that point of `s`.
 hipError_t rti::join_gather(rt_comm c, hipStream_t s) {
     hipError_t e = hipSetDevice(c->ctx->device);
-    for (int q = 0; q < c->nranks && e == hipSuccess; ++q)
+    for (int q = 0; c->ipc_linked && q < c->nranks && e == hipSuccess; ++q)
         if (q != c->root) e = hipStreamWaitValue64(s, c->rflags + q, c->join_seq, hipStreamWaitValueGte, ~0ull);
+    for (size_t j = 0; j < c->join_events.size() && e == hipSuccess; ++j) e = hipStreamWaitEvent(s, c->join_events[j], 0);
     if (e == hipSuccess && c->sends) e = hipStreamWaitEvent(s, c->dsent, 0);
     if (e == hipSuccess) e = hipEventRecord(c->ctx->gtail, s);
     return e;
