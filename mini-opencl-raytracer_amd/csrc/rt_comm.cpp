@@ -1228,7 +1228,7 @@ int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
     if (R) {
         R->join_seq = R->seq;
         R->join_events.clear();
-XX
+        if (!R->ipc_linked && !R->members && n_local > 1) {  // (no member list: join now, on the root's stream)
             hipError_t e = hipSetDevice(R->ctx->device);
             for (int j = 0; j < n_local && e == hipSuccess; ++j)
                 if (comms[j] != R) e = hipStreamWaitEvent(R->ustream, comms[j]->sent[comms[j]->slot ^ 1], 0);
