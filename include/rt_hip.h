@@ -311,13 +311,7 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     or a device pointer of one of its buffers
  *                                     (rtBufferGetDevicePointer) has been handed out, the host may
  *                                     synchronise outside the library, so from then on every
- *                                     rtEnqueueKernel launches at once.
- *   SPEC_WALK                         step schedule, LDS octant walk, builds with the speculative
- *                                     walk compiled in (RT_SPEC=1; the shipped build has it out,
- *                                     measured slower): 1 (default) = speculative walk (a lane
- *                                     walks on past a passed leaf while its triangles are pending;
- *                                     same bits), 0 = the plain walk.  Trees whose child boxes do
- *                                     not nest in their parents' always walk plainly. */
+ *                                     rtEnqueueKernel launches at once. */
 enum rt_tuning {
     RT_TUNE_REFILL_MIN = 0,
     RT_TUNE_SHADE_MIN = 1,
@@ -339,7 +333,7 @@ enum rt_tuning {
     RT_TUNE_PERFRAME_DEFER = 19,
     RT_TUNE_MAX_BLOCKS = 20,
     RT_TUNE_PERFRAME_DEFER_MIN = 21,
-    RT_TUNE_SPEC_WALK = 22,
+    /* 22: the retired speculative walk's switch (RT_INVALID_VALUE) */
     RT_TUNE_PERFRAME_BATCH = 23
 };
 int rtKernelSetTuning(rt_kernel k, int param, int value);

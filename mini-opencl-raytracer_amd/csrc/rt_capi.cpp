@@ -127,8 +127,6 @@ struct rt_kernel_s {
     float4* shade_mats = nullptr;      // compact materials
     size_t shade_tris_cap = 0, shade_mats_cap = 0;
     bool oct_ok = false;               // every leaf fits the records' inline {first, count}
-    bool nested = false;               // every child box lies inside its parent's (speculative walk)
-    int spec_walk = 1;                 // RT_TUNE_SPEC_WALK
     float4* g_nodes = nullptr;         // global-scene node records (64 B, top of the tree first)
     size_t g_nodes_cap = 0;
     uint32_t n_top = 0, top_limit = 384;  // nodes of g_nodes staged in LDS (global path; swept, profiles/r01/bunny_top_nodes_sweep_2.txt)
@@ -232,25 +230,6 @@ int check_nodes(const rt_cl_bvh_node* nd, uint32_t n, uint32_t n_tris, int* dept
     // The reference's 64-entry stack (kernel_bvh.cl:181) would overflow past depth 64; the
     // stackless walk here has no such limit, so deeper trees are rendered, not rejected.
     return RT_SUCCESS;
-}
-
-// The speculative walk (rt_kernels_body.hpp, step_body) needs every interior node's box to hold
-// its children's: then a child whose box a ray passes at some t has every ancestor passed at that
-// t too (the slab arithmetic is monotone in the planes and in t), which is what lets a lane walk
-// ahead of a pending leaf and re-test only the node it stops at.  The reference's builder forms
-// parents as unions of their children (CLBVHnode.cpp:7-159, CLmathlib.hpp:190-204), and so do
-// rtBuildBVH's; a hand-made tree that breaks it (or holds NaN planes) is walked plainly.
-bool boxes_nest(const rt_cl_bvh_node* nd, uint32_t n) {
-    auto inside = [](const rt_cl_bvh_node& c, const rt_cl_bvh_node& p) {
-        return c.bounds.pmin.x >= p.bounds.pmin.x && c.bounds.pmin.y >= p.bounds.pmin.y &&
-               c.bounds.pmin.z >= p.bounds.pmin.z && c.bounds.pmax.x <= p.bounds.pmax.x &&
-               c.bounds.pmax.y <= p.bounds.pmax.y && c.bounds.pmax.z <= p.bounds.pmax.z;
-    };
-    for (uint32_t i = 0; i < n; ++i) {
-        if (nd[i].nPrimitives > 0) continue;
-        if (!inside(nd[i + 1], nd[i]) || !inside(nd[nd[i].offset], nd[i])) return false;
-    }
-    return true;
 }
 
 // Per-octant skip pointers (see rt_kernels.hip, intersect): for octant o (bit i = the ray
@@ -540,7 +519,6 @@ int prepare_scene(rt_kernel k) {
     k->n_mats = nmat;
     k->depth = depth;
     k->oct_ok = oct_ok;
-    k->nested = boxes_nest(reinterpret_cast<const rt_cl_bvh_node*>(nb), nn);
     k->n_top = n_top;
     k->packed_for_tris = tm;
     k->packed_tris_gen = tm->generation;
@@ -645,7 +623,6 @@ int rtCreateContext(int device_index, rt_context* out) {
             c->n_xcd = 8;
     }
     if (c->num_cus <= 0) c->num_cus = 256;
-    c->render_cus = c->num_cus;
     *out = c;
     return RT_SUCCESS;
 }
@@ -1121,14 +1098,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds && RT_RAY_RING ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
+                 (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
                  (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end
-    a.flagTiles = fused && !wf && si == RT_SCHED_STEP && ((lds && RT_RAY_RING) || (goct && RT_STEAL && RT_GOCT_TILE_FLAGS)) ? 1u
-                  : fused && !wf && si == RT_SCHED_STEP && goct && RT_GOCT_NOFLAGS ? 2u : 0u;
-    a.specWalk = k->spec_walk && k->nested ? 1u : 0u;
+    a.flagTiles = fused && !wf && si == RT_SCHED_STEP && lds ? 1u : fused && !wf && si == RT_SCHED_STEP && goct ? 2u : 0u;
 
     const int mi = k->math;
     const bool bofs = lds && a.octB == rtk::kOctB;
@@ -1139,10 +1114,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct);
         k->occ_smem[si][mi][lds][k->stats][var] = smem;
     }
-    // (a render stream may exclude CUs an RCCL communicator reserved: rti::reserve_cus)
-    const bool on_rstream = rstr != ctx->stream;
-    uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) *
-                    (uint64_t)(on_rstream ? ctx->render_cus : ctx->num_cus);
+    uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) * (uint64_t)ctx->num_cus;
     // tiles: one workgroup per 16x16 tile at most; persistent schedules: one 8x8 tile per wave
     // (wavefront extend: 8 waves per workgroup)
     grid = std::min<uint64_t>(grid, si == RT_SCHED_TILES ? n_tiles
@@ -1623,42 +1595,6 @@ int rtContextGetStream(rt_context ctx, void** s) {
 
 }  // extern "C"
 
-namespace rti {
-
-int reserve_cus(rt_context ctx, int per_xcd, std::vector<uint32_t>* comm_mask) {
-    const int per = ctx->num_cus / ctx->n_xcd;
-    if (per_xcd < 0 || per_xcd >= per) return RT_INVALID_VALUE;
-    const size_t words = (size_t)(ctx->num_cus + 31) / 32;
-    std::vector<uint32_t> all(words, 0u), res(words, 0u);
-    for (int b = 0; b < ctx->num_cus; ++b) {
-        all[b / 32] |= 1u << (b % 32);
-        // the last per_xcd CUs of each XCD: bit = cu * n_xcd + xcd
-        if (b / ctx->n_xcd >= per - per_xcd) res[b / 32] |= 1u << (b % 32);
-    }
-    if (comm_mask) *comm_mask = res;
-    if (per_xcd == ctx->reserved_per_xcd) return RT_SUCCESS;
-    // re-create the render streams on the remaining CUs, once their work is done
-    hipError_t e = hipSuccess;
-    for (hipStream_t& r : ctx->rstream) {
-        if (e == hipSuccess) e = hipStreamSynchronize(r);
-        if (e != hipSuccess) break;
-        (void)hipStreamDestroy(r);
-        r = nullptr;
-        if (per_xcd == 0) {
-            e = hipStreamCreateWithFlags(&r, hipStreamNonBlocking);
-        } else {
-            std::vector<uint32_t> m(words);
-            for (size_t w = 0; w < words; ++w) m[w] = all[w] & ~res[w];
-            e = hipExtStreamCreateWithCUMask(&r, (uint32_t)words, m.data());
-        }
-    }
-    if (e != hipSuccess) return map_hip(e);
-    ctx->reserved_per_xcd = per_xcd;
-    ctx->render_cus = ctx->num_cus - per_xcd * ctx->n_xcd;
-    return RT_SUCCESS;
-}
-
-}  // namespace rti
 
 extern "C" {
 
@@ -1707,7 +1643,6 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_GLOBAL_OCT: if (!in(0, 1)) return RT_INVALID_VALUE; k->global_oct = value; break;
         case RT_TUNE_PERFRAME_DEFER: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_defer = value; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: if (value < 0) return RT_INVALID_VALUE; k->pf_defer_min = (uint32_t)value; break;
-        case RT_TUNE_SPEC_WALK: if (!in(0, 1)) return RT_INVALID_VALUE; k->spec_walk = value; break;
         case RT_TUNE_PERFRAME_BATCH: if (!in(1, (int)rtk::kMaxFusedFrames)) return RT_INVALID_VALUE; k->pf_batch = (uint32_t)value; break;
         default: return RT_INVALID_VALUE;
     }
@@ -1737,7 +1672,6 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_GLOBAL_OCT: *value = k->global_oct; break;
         case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: *value = (int)k->pf_defer_min; break;
-        case RT_TUNE_SPEC_WALK: *value = k->spec_walk; break;
         case RT_TUNE_PERFRAME_BATCH: *value = (int)k->pf_batch; break;
         default: return RT_INVALID_VALUE;
     }

@@ -132,7 +132,6 @@ struct rt_comm_s {
     // loopback worlds (rtCommInitLoopback): no RCCL; `group` identifies the world (shared by its
     // members), whose gathers always run on the copy engines with the members linked by address
     const void* group = nullptr;
-    bool reserved = false;      // holds a CU reservation on ctx (rti::reserve_cus)
     int rank = 0, nranks = 1;
     hipStream_t cstream = nullptr;  // transfers (copy engines or RCCL), RCCL setup and reductions
     hipStream_t ustream = nullptr;  // root: releases (copy engines), unpack (RCCL)
@@ -239,60 +238,32 @@ int shared_world_id(rt_comm c) {
     }
 }
 
-// The communicator's transfer and unpack streams run at the device's greatest stream priority.
-// Two reasons, both read off a kernel trace of the world-1 flow (profiles/r04/dist_flow_ab.txt):
-// * HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES 4); at normal priority these two
-//   shared the main stream's and a render stream's queue, so the next fused render sat behind the
-//   previous step's unpack, which sat behind its transfer.  High-priority streams get queues of
-//   their own.
-// * RCCL's transfer kernel needs CU slots, and a persistent render holds them all until it
-//   drains; at high priority its workgroups are dispatched first -- which still leaves it waiting
-//   for a drain (hence the copy-engine transport).
-#ifndef RT_COMM_STREAM_PRIO
-#define RT_COMM_STREAM_PRIO 1
-#endif
-// RCCL communicators: CUs of every XCD kept for the communicator's streams (rti::reserve_cus),
-// an A/B knob of the RCCL transport.  RCCL's transfer kernel (64 workgroups of 256 threads, 37 KB
-// of LDS and 248 VGPRs each on gfx950) fits beside a persistent render on no CU; with a
-// reservation it runs at once on its own CUs, but the renders lose those CUs' share and the
-// world-1 flow measured slower than without (0.85 vs 0.82 ms/frame, profiles/r04/dist_flow_ab.txt).
-// 0 = none (default).
+// The communicator's streams (transfer, root, and the extra transfer streams) run at the device's
+// greatest stream priority.  Read off a kernel trace of the world-1 flow
+// (profiles/r04/dist_flow_ab.txt): HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES
+// 4); at normal priority the communicator's streams shared the main stream's and a render stream's
+// queue, so the next fused render sat behind the previous step's gather.  High-priority streams
+// get queues of their own.  (Reserving CUs per XCD for RCCL's transfer kernel let it run at once
+// but cost the renders more than it saved -- 0.85 vs 0.82 ms/frame in the same flow; removed in
+// round 5.)
 int comm_events(rt_comm c, hipError_t e);
-#ifndef RT_COMM_RESERVE_PER_XCD
-#define RT_COMM_RESERVE_PER_XCD 0
-#endif
-int comm_streams(rt_comm c, bool rccl) {
-    hipError_t e = hipSuccess;
-    if (rccl && RT_COMM_RESERVE_PER_XCD > 0) {
-        std::vector<uint32_t> mask;
-        int rc = rti::reserve_cus(c->ctx, RT_COMM_RESERVE_PER_XCD, &mask);
-        if (rc) return rc;
-        c->reserved = true;
-        ++c->ctx->reserve_refs;
-        e = hipExtStreamCreateWithCUMask(&c->cstream, (uint32_t)mask.size(), mask.data());
-        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->ustream, (uint32_t)mask.size(), mask.data());
-        return comm_events(c, e);
-    }
+int comm_streams(rt_comm c) {
     int least = 0, greatest = 0;
-    e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const int prio = RT_COMM_STREAM_PRIO ? greatest : least;
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, prio);
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, greatest);
     return comm_events(c, e);
 }
 
 #ifndef RT_COMM_XFER_STREAMS
 #define RT_COMM_XFER_STREAMS 2  // 1: the copies on the communicator stream itself
 #endif
-#ifndef RT_COMM_XFER_PRIO
-#define RT_COMM_XFER_PRIO 1     // extra transfer streams at the greatest priority (own hardware queues)
-#endif
 static_assert(RT_COMM_XFER_STREAMS >= 1 && RT_COMM_XFER_STREAMS <= 8, "copy streams");
 int comm_events(rt_comm c, hipError_t e) {
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     for (int i = 0; RT_COMM_XFER_STREAMS > 1 && i < RT_COMM_XFER_STREAMS && e == hipSuccess; ++i) {
-        e = hipStreamCreateWithPriority(&c->xstream[i], hipStreamNonBlocking, RT_COMM_XFER_PRIO ? greatest : least);
+        e = hipStreamCreateWithPriority(&c->xstream[i], hipStreamNonBlocking, greatest);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xdone[i], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xgo, hipEventDisableTiming);
@@ -405,8 +376,6 @@ void release(rt_comm c) {
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
-    // the last communicator of the context gives its CUs back to the renders
-    if (c->reserved && --c->ctx->reserve_refs == 0) (void)rti::reserve_cus(c->ctx, 0, nullptr);
     // a shared world's rank removes its own exchange files but the last: every rank wrote its file
     // of exchange k only after reading all files of exchange k - 1, so those have all been read;
     // the last one may still be awaited by a slower rank (the caller removes the directory)
@@ -776,7 +745,7 @@ int rtCommInitRank(rt_context ctx, int nranks, const void* id, int rank, rt_comm
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     int rc = map_nccl(ncclCommInitRank(&c->nc, nranks, u, rank));
-    if (!rc) rc = comm_streams(c, true);
+    if (!rc) rc = comm_streams(c);
     if (rc) {
         release(c);
         return rc;
@@ -805,7 +774,7 @@ int rtCommInitAll(const rt_context* ctxs, int n, rt_comm* comms_out) {
             c->rank = i;
             c->nranks = n;
             (void)hipSetDevice(ctxs[i]->device);
-            rc = comm_streams(c, true);
+            rc = comm_streams(c);
         } else {
             (void)ncclCommDestroy(nc[i]);
             nc[i] = nullptr;
@@ -845,7 +814,7 @@ int rtCommInitLoopback(const rt_context* ctxs, int n, rt_comm* comms_out) {
             c->rank = i;
             c->nranks = n;
             hipError_t e = hipSetDevice(ctxs[i]->device);
-            rc = e == hipSuccess ? comm_streams(c, false) : map_hip(e);
+            rc = e == hipSuccess ? comm_streams(c) : map_hip(e);
         }
         if (rc) {
             if (c) release(c);
@@ -884,7 +853,7 @@ int rtCommInitShared(rt_context ctx, int nranks, int rank, const char* dir, rt_c
         delete c;
         return rc;
     }
-    rc = comm_streams(c, false);
+    rc = comm_streams(c);
     if (rc) {
         release(c);
         return rc;

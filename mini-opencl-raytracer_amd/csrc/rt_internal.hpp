@@ -20,14 +20,9 @@ struct rt_context_s {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 0;
-    // CUs the render streams (rstream) may use: num_cus, unless an RCCL communicator reserved some
-    // for its transfer kernels (rti::reserve_cus); fused renders size their persistent grid by it
-    int render_cus = 0;
-    int reserved_per_xcd = 0;
-    int reserve_refs = 0;  // communicators holding the reservation
     int n_xcd = 1;  // XCDs (CU-mask bit b selects CU b / n_xcd of XCD b % n_xcd)
     // Fused frames: the accumulation launch runs on its own stream, so it overlaps the next
-    // render (its waves fit beside the render grid: RT_ACCUM_VGPRS).  Every other operation
+    // render (its waves fit beside the render grid: 32 VGPRs).  Every other operation
     // goes through qs(), which first makes the context's in-order stream wait for the
     // accumulations enqueued so far -- to the caller the context stays one in-order queue.
     hipStream_t astream = nullptr;
@@ -146,13 +141,9 @@ inline hipStream_t qs(rt_context ctx) {
 }
 
 // Make `s` wait for everything enqueued on the main stream so far.  The main stream's tail is
-// re-recorded only when something may have been enqueued there since the last record
-// (RT_MTAIL_ALWAYS: every time, the round-3 behaviour, kept for A/B builds).
+// re-recorded only when something may have been enqueued there since the last record.
 inline hipError_t main_tail_wait(rt_context ctx, hipStream_t s) {
-#ifndef RT_MTAIL_ALWAYS
-    if (ctx->mdirty || ctx->mexposed)
-#endif
-    {
+    if (ctx->mdirty || ctx->mexposed) {
         const hipError_t e = hipEventRecord(ctx->mtail, ctx->stream);
         if (e != hipSuccess) return e;
         ctx->mdirty = false;
@@ -174,10 +165,5 @@ void unpin(rt_mem m);  // rt_capi.cpp: frees a released buffer on its last unpin
 // rtCommShardKernel's interleave (rt_capi.cpp): refused for a kernel with a work range
 int shard_kernel(rt_kernel k, unsigned period, unsigned phase);
 
-// Reserve `per_xcd` CUs of every XCD for a communicator (rt_capi.cpp): the context's render
-// streams are re-created without them (after draining), fused renders size their grid to the
-// rest, and `comm_mask` receives the reserved CUs' mask for the communicator's streams
-// (hipExtStreamCreateWithCUMask words).  per_xcd 0 releases the reservation.
-int reserve_cus(rt_context ctx, int per_xcd, std::vector<uint32_t>* comm_mask);
 
 }  // namespace rti

@@ -26,13 +26,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOC
 void kernel_entry_step_devicelib_goct(KernelArgs a) {
     step_body<MathDeviceLib, true, kStats, false, true>(a);
 }
-#ifdef RT_STEP_PINNED_WAVES
-#define RT_STEP_PINNED_OCC __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
-#else
-#define RT_STEP_PINNED_OCC
-#endif
 template <bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct = false>
-__global__ __launch_bounds__(256) RT_STEP_PINNED_OCC void kernel_entry_step_pinned(KernelArgs a) {
+__global__ __launch_bounds__(256) void kernel_entry_step_pinned(KernelArgs a) {
     step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct>(a);
 }
 
@@ -115,7 +110,7 @@ __global__ void accum_key(KernelArgs a, uint32_t* key) {
 
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st) {
     if (math == MathShipped::kId) return launch_accum_frames_shipped(a, key, st);
-    const dim3 grid((a.nTiles + kAccumWgWaves * kAccumTilesPerWave - 1u) / (kAccumWgWaves * kAccumTilesPerWave));
+    const dim3 grid((a.nTiles + kAccumWgWaves - 1u) / kAccumWgWaves);
     if (math == MathDeviceLib::kId) {
         hipLaunchKernelGGL(accum_key<MathDeviceLib>, dim3(1), dim3(64), 0, st, a, key);
         hipLaunchKernelGGL(accum_frames<MathDeviceLib>, grid, dim3(64 * kAccumWgWaves), 0, st, a, key);

@@ -46,16 +46,14 @@ struct KernelArgs {
     // launch; radiance per (frame slot, gid) in radBuf[slot * radStride + gid] (null: one frame)
     float4* radBuf;
     // primary-miss flags: 1 = radiance (K_rad x3), not in radBuf.  flagTiles 0: one byte per
-    // [slot * radStride + gid]; flagTiles 1 (the LDS walk's ray ring, and -- RT_GOCT_TILE_FLAGS --
-    // the HBM/L2 octant walk, which hands out each tile's work items from one wave): one 64-bit
-    // word per [slot * nTiles + tile], bit = pixel's lane in the tile, written once by the wave
-    // that handed the tile out; every path not decided at its camera ray stores its radiance.
-    // flagTiles 2 (the HBM/L2 octant walk, RT_GOCT_NOFLAGS): no flags, every path stores it
+    // [slot * radStride + gid]; flagTiles 1 (the LDS walk's ray ring): one 64-bit word per
+    // [slot * nTiles + tile], bit = pixel's lane in the tile, written once by the wave that
+    // generated the tile's camera rays; every path not decided at its camera ray stores its
+    // radiance.  flagTiles 2 (the HBM/L2 octant walk): no flags, every path stores it
     uint8_t* frameFlags;
     uint32_t flagTiles;
     uint32_t nFrames, radStride;
     uint32_t tileMajor;                 // fused: work items ordered (tile, frame) instead of (frame, tile)
-    uint32_t specWalk;                  // step schedule, octant walks: speculative walk (boxes nest)
     // per-frame launches (step schedule): sky-pixel shortcut key, chained launch to launch --
     // pfKeyIn = the value all-sky pixels hold if they followed the chain, pfKeyOut = this launch's
     const uint32_t* pfKeyIn;
@@ -72,29 +70,14 @@ constexpr int kNumSched = 5;
 constexpr uint32_t kMaxFusedFrames = 8;
 // step schedule LDS per wave: the finish queue, 64 x {radiance, gid}
 constexpr uint32_t kFinishWaveBytes = 64u * 16u;
-#ifndef RT_RAY_RING
-#define RT_RAY_RING 1
-#endif
 // step schedule, LDS scenes: per-wave ring of camera rays generated a whole 8x8 tile at a time
 // ({dir, seed}, {invDir, sign} (fused launches) + work-item id per slot)
 constexpr uint32_t kRingSlots = 64;
 constexpr uint32_t kRingWaveBytes = kRingSlots * 32u + kRingSlots * 4u;
 constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // per-frame: no invDir
-// step schedule, LDS scenes: per workgroup, each wave's remaining chunk {next, end} (64-bit word
-// per wave), from which its siblings take single tiles once the work counter is dry
-#ifndef RT_STEAL
-#define RT_STEAL 1
-#endif
-// fused HBM/L2 octant walks: primary misses decided at refill, flags as one 64-bit word per
-// (frame, tile) (step_body, kGoctTiles); 0 = a flag byte per path
-#ifndef RT_GOCT_TILE_FLAGS
-#define RT_GOCT_TILE_FLAGS 0
-#endif
-// fused HBM/L2 octant walks: no flags at all -- every path stores its radiance (flagTiles 2)
-#ifndef RT_GOCT_NOFLAGS
-#define RT_GOCT_NOFLAGS 1
-#endif
-constexpr uint32_t kStealBytes = RT_STEAL ? 4u * 8u + 32u : 0u;  // (padded to whole float4s)
+// step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
+// from which its siblings take single tiles once the work counter is dry
+constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address

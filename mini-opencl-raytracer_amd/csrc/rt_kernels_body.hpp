@@ -15,7 +15,7 @@
 //     ray's octant, so it is replayed exactly with per-octant skip pointers (8 per
 //     node, built on the host): node visits, triangle tests and their order are the
 //     reference's, without LDS pushes/pops or the dependent pop latency;
-//   * traversal keeps {t, primitive, u, v} (RT_KEEP_UV); the hit record (position, shading
+//   * traversal keeps {t, primitive, u, v}; the hit record (position, shading
 //     normal, material) is formed once after the walk from the last accepted triangle, which
 //     yields the same values as the reference forming it at every accept;
 //   * no MFMA: this is branchy, latency-bound traversal.
@@ -268,23 +268,6 @@ __device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelAr
     t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
     skip = __float_as_uint(B.w);
     return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
-}
-
-// The same visit for the speculative walk (step_body, kSpec): `hit` and the record's two links.
-template <bool kBofs>
-__device__ __forceinline__ bool oct_probe(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
-                                          float t, uint32_t& hn, uint32_t& mn) {
-    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
-    const float4 A = sc.onodes[i], B = sc.onodes[i + (kBofs ? kOctB : a.octB)];
-    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
-    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
-    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
-    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
-    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
-    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
-    hn = __float_as_uint(B.z);
-    mn = __float_as_uint(B.w);
-    return t1 >= t0;
 }
 
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
@@ -619,23 +602,17 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
 // streamed past the caches (nontemporal) where the render reads its scene through them (HBM/L2
 // scene path: bunny proxy 1.425 -> 1.404 ms/frame, profiles/r02/nt_rad_ab.txt; the LDS path
 // showed no gain for its stores)
-#ifndef RT_NT_RAD
-#define RT_NT_RAD 1
-#endif
 typedef float rad_v4f __attribute__((ext_vector_type(4)));
 template <bool kNt>
 __device__ __forceinline__ void rad_store(float4* p, float x, float y, float z) {
-    if (RT_NT_RAD && kNt)
+    if (kNt)
         __builtin_nontemporal_store(rad_v4f{x, y, z, 0.0f}, reinterpret_cast<rad_v4f*>(p));
     else
         *p = make_float4(x, y, z, 0.0f);
 }
 __device__ __forceinline__ float4 rad_load(const float4* p) {
-    if (RT_NT_RAD) {
-        const rad_v4f v = __builtin_nontemporal_load(reinterpret_cast<const rad_v4f*>(p));
-        return make_float4(v.x, v.y, v.z, v.w);
-    }
-    return *p;
+    const rad_v4f v = __builtin_nontemporal_load(reinterpret_cast<const rad_v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
 }
 
 __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
@@ -674,15 +651,9 @@ __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, 
 // t, hit and pixel -- is exactly the reference's.
 constexpr uint32_t kIdle = 0, kTrav = 1, kLeaf = 2, kShade = 3, kDone = 4;
 constexpr uint32_t kNotWalking = 0x80000000u;  // LDS path walk word outside TRAV
-// speculative walk compiled in (RT_TUNE_SPEC_WALK then picks it per kernel).  Off: on the 4K
-// Cornell headline the build with it ran 0.824 ms/frame speculating and 0.841 with the knob at 0,
-// against 0.767 without the code (profiles/r04/spec_walk_ab.txt)
-#ifndef RT_SPEC
-#define RT_SPEC 0
-#endif
-#ifndef RT_SPEC_STATS
-#define RT_SPEC_STATS 0  // diagnostic: counting builds walk speculatively too (visits = a superset)
-#endif
+// (A speculative walk -- a lane passing a leaf walks on to the next leaf while its triangles wait
+// -- was built and measured slower in round 4: 0.824 vs 0.767 ms/frame on the 4K Cornell
+// headline; removed in round 5, its record is profiles/r04/spec_walk_ab.txt.)
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -705,13 +676,7 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 // steps of the chosen kind per scheduling decision (thresholds are re-checked after each
 // burst): the per-step ballots and threshold tests cost about as much as a node visit
 #ifndef RT_PRIO_SHADE
-#define RT_PRIO_SHADE 1  // LDS path: wave priority while shading (traversal steps run at 3)
-#endif
-#ifndef RT_PRIO_REFILL
-#define RT_PRIO_REFILL -1  // LDS path: wave priority during finish + refill (-1: as shading left it)
-#endif
-#ifndef RT_GPHASE
-#define RT_GPHASE 1  // global path: phase priorities (traversal 3 / shading 1) instead of a fixed 1
+#define RT_PRIO_SHADE 1  // wave priority while shading, finishing and refilling (traversal steps run at 3)
 #endif
 #ifndef RT_NODE_BURST
 #define RT_NODE_BURST 7  // LDS walk (6 before work stealing; 5 / 8 slower: profiles/r03/burst_sweep.txt)
@@ -724,20 +689,10 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
 #endif
-// step schedule: keep the accepted triangle's barycentrics during the walk (2 registers, 2 selects
-// per test) instead of re-evaluating them at shading (with_uv, 0): the same values bit for bit (the
-// accepted test computed them); 4K Cornell 0.777 -> 0.773, bunny proxy 1.376 -> 1.364 ms/frame
-// (profiles/r04/keep_uv_ab.txt)
-#ifndef RT_KEEP_UV
-#define RT_KEEP_UV 1
-#endif
-// shade early when at most RT_TRAV_LOW lanes are still walking and at least RT_SHADE_LOW wait
-#ifndef RT_TRAV_LOW
-#define RT_TRAV_LOW 0
-#endif
-#ifndef RT_SHADE_LOW
-#define RT_SHADE_LOW 24
-#endif
+// (The step schedule keeps the accepted triangle's barycentrics during the walk rather than
+// re-evaluating them at shading: same bits, 4K Cornell 0.777 -> 0.773, bunny proxy 1.376 -> 1.364
+// ms/frame, profiles/r04/keep_uv_ab.txt.  Shading early once few lanes still walk lost 2.5 %,
+// profiles/r04/early_shade_ab.txt: removed in round 5.)
 
 
 // the same for scenes read from HBM/L2 (global path)
@@ -811,16 +766,16 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const bool fused = a.radBuf != nullptr;
     // the waves' remaining chunks (work stealing, take_tile): empty ranges before anyone looks
     unsigned long long* steal = nullptr;
-    if (RT_STEAL) {
+    {
         extern __shared__ __attribute__((aligned(16))) float4 smem_s[];
-        constexpr bool kRingLds = RT_RAY_RING && kLdsScene && !kGlobalOct;
+        constexpr bool kRingLds = kLdsScene && !kGlobalOct;
         steal = reinterpret_cast<unsigned long long*>(
             smem_s + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
             (kRingLds ? 4u * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u) : 0u));
         if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
     }
     const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
-    if (RT_STEAL && kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
+    if (kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
     const F3 camFront{a.camFront[0], a.camFront[1], a.camFront[2]};
@@ -852,7 +807,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* fq = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (uint32_t)(tid >> 6) * kFinishSlots;
     uint32_t fq_n = 0;  // wave-uniform
-#if RT_RAY_RING
     // LDS scenes: per-wave ring of camera rays, generated one whole 8x8 tile (64 lanes) at a
     // time and handed to idle lanes at refill -- create_ray then runs on full waves instead of
     // on the few lanes a refill serves.  Same rays, same seeds, same pixel order.
@@ -865,11 +819,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                      (uint32_t)(tid >> 6) * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u);
     float4* ring_i = ring_d + kRingSlots;
     uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (fused ? 2u : 1u) * kRingSlots);
-#else
-    constexpr bool kRing = false;
-    float4* ring_d = nullptr;
-    uint32_t* ring_g = nullptr;
-#endif
     uint32_t rc_head = 0, rc_n = 0;  // wave-uniform: ring entries [rc_head, rc_head + rc_n)
     bool dry = false;                // wave-uniform: the work counter is exhausted
 
@@ -885,44 +834,18 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // at after the leaf, `leaf_i` the leaf's next triangle.
     uint32_t cur = kLdsScene ? kNotWalking : 0u;
     uint32_t leaf_i = 0u, leaf_end = 0;
-    // Speculative walk (octant walks; counting builds keep the plain walk, whose node visits are
-    // the reference's one for one).  A lane that passes a leaf does not wait there for a triangle
-    // step: the leaf's code goes to `pend` (tested by later triangle steps, one triangle each) and
-    // the walk goes on at the leaf's skip pointer with the t it has, until it passes a second leaf
-    // -- there it stops (cur = that leaf's code, >= kLeafMin; leaf_i = its node) until `pend` is
-    // done, then re-visits that node with the updated t.  So a lane in a leaf still takes node steps, and a walking
-    // lane with a pending leaf still takes triangle steps.  Same triangle tests in the same order
-    // at the same t as the reference (kernel_bvh.cl:171-219), hence the same bits: t only
-    // decreases, a box test is monotone in t and children's boxes nest in their parents'
-    // (CLBVHnode.cpp:7-159 builds them as unions), so every node the reference enters after the
-    // pending leaf the walk enters too, every leaf it skipped on the way fails for the reference
-    // as well, and the stop node is re-tested at the reference's t before its triangles.  Extra
-    // work: node visits the reference would have skipped (rt_capi.cpp checks the nesting on the
-    // host and walks plainly when a tree breaks it).
-    // (LDS scenes only: on the octant walk over HBM/L2 the extra visits cost address-unit load
-    // instructions, that walk's binding resource -- bunny proxy +12 %, profiles/r04/spec_walk.txt)
-    constexpr bool kSpec = RT_SPEC && kLdsScene && !kGlobalOct && (!kStats || RT_SPEC_STATS);
-    uint32_t pend = 0u;  // (kSpec) pending leaf code count << 24 | first while >= kLeafMin
-    // fused HBM/L2 octant walks (a.flagTiles): camera rays that miss the root box are decided at
-    // refill, as the ray ring does for LDS scenes, and each tile's primary-miss flags go out as one
-    // 64-bit word when its wave has handed out the tile's last work item (tile_sky accumulates
-    // them): no flag byte per path.  A byte per path, merged in L2 from scattered stores, left as
-    // 32-B partial-line writes: 0.45 of the bunny launch's 1.49 GB (profiles/r04/goct_flags.txt)
-    // (measured 1 % slower on the bunny proxy than the byte flags: the root visit at refill costs
-    // load instructions outside the node bursts -- off, RT_GOCT_TILE_FLAGS)
-    const bool kGoctTiles = RT_GOCT_TILE_FLAGS && kGlobalOct && RT_STEAL && fused && a.flagTiles == 1u;
     // fused HBM/L2 octant walks without flags (a.flagTiles 2, the default there): every path
     // stores its radiance, primary misses included, and the accumulation reads every frame -- the
     // flag byte per path is gone (0.45 GB of 32-B partial-line writes per bunny launch)
+    // (Per-tile flag words decided at refill measured 1 % slower there: the root visit at refill
+    // costs load instructions outside the node bursts, profiles/r04/goct_flags.txt.)
     const bool kNoFlags = kGlobalOct && fused && a.flagTiles == 2u;
-    [[maybe_unused]] unsigned long long tile_sky = 0ull;  // wave-uniform
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
-    [[maybe_unused]] uint32_t chunk_used = 0;  // wave-uniform (without work stealing)
     bool chunk_tail = a.chunkSplit == 0u;                     // wave-uniform: no bulk region
     bool exhausted = false;                    // wave-uniform
-    [[maybe_unused]] uint32_t tile_unit = 0, tile_used = 64;  // wave-uniform (work stealing, HBM/L2 scene paths)
+    uint32_t tile_unit = 0, tile_used = 64;    // wave-uniform (HBM/L2 scene paths: the current tile)
     // diagnostic phase timers (stats variant only): shader-clock cycles per phase, per wave
     uint64_t cyc_refill = 0, cyc_trav = 0, cyc_shade = 0;
     const uint64_t cyc_start = kStats ? __builtin_amdgcn_s_memtime() : 0;
@@ -936,7 +859,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 
     for (;;) {
         // ---- finish + refill: accumulate finished paths, start new pixels ----------------------
-        if (kLdsScene && RT_PRIO_REFILL >= 0) __builtin_amdgcn_s_setprio(RT_PRIO_REFILL);
         uint64_t tA = kStats ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t n_free = popc_ballot(state == kIdle || state == kDone);
         if (n_free == 64u || (!exhausted && n_free >= kRefillMin)) {
@@ -955,8 +877,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     // (ray ring: the tile's flags were written when it was generated -- a
                     // path that still ends as K_rad stores its radiance like any other, which
                     // the accumulation reads to the same bits)
-                    if (!skyv || kRing || kGoctTiles || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
-                    if (!kRing && !kGoctTiles && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
+                    if (!skyv || kRing || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
+                    if (!kRing && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
             }
@@ -999,19 +921,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 if (idle == 0ull) break;
                 if (rc_n == 0u) {
                     uint32_t unit = 0;  // the tile's first work item in the work order (wave-uniform)
-#if RT_STEAL
                     if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
                                    chunk_tail, dry, unit)) {
-#else
-                    if (!dry && chunk_used >= chunk_len) {
-                        if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail))
-                            dry = true;
-                        else
-                            chunk_used = 0;
-                    }
-                    unit = chunk_base + chunk_used;
-                    if (dry) {
-#endif
                         exhausted = true;
 #if RT_TIMELINE
                         rt_dry = __builtin_amdgcn_s_memrealtime();
@@ -1086,9 +997,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     }
                     rc_head = 0;
                     rc_n = (uint32_t)__popcll(vm);
-#if !RT_STEAL
-                    chunk_used += 64u;
-#endif
                     continue;
                 }
                 const uint32_t rank = lane_rank(idle);
@@ -1129,7 +1037,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             while (!kRing && !exhausted) {
                 const unsigned long long idle = __ballot(state == kIdle);
                 if (idle == 0ull) break;
-#if RT_STEAL
                 // tile_unit: the current tile's first work item, tile_used of its 64 handed out
                 if (tile_used >= 64u) {
                     if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
@@ -1140,16 +1047,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     tile_used = 0;
                 }
                 const uint32_t used = tile_used, unit = tile_unit;
-#else
-                if (chunk_used >= chunk_len) {
-                    if (!next_chunk(a, total, (uint32_t)lane, chunk_base, chunk_len, chunk_tail)) {
-                        exhausted = true;
-                        break;
-                    }
-                    chunk_used = 0;
-                }
-                const uint32_t used = chunk_used & 63u, unit = (chunk_base + chunk_used) & ~63u;
-#endif
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), 64u - used);  // within one 8x8 tile
@@ -1166,7 +1063,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     slot = tile / a.nTiles;
                     tile -= slot * a.nTiles;
                 }
-                bool sky = false;
                 if (state == kIdle && rank < take) {
                     const uint32_t w = used + rank;  // chunks are whole 8x8 tiles
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
@@ -1187,27 +1083,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
                             cur = 0;
                             if (kStats) ++st.rays;
-                            if (kGoctTiles) {
-                                // the walk's first visit (the root, t = kMaxDist) made here: a miss
-                                // is a primary miss (Intersect finds nothing, the bounce adds the
-                                // sky and breaks, Render returns K_rad: kernel_bvh.cl:358-361,
-                                // :383) -- flagged, no path; a hit continues at the root's successor
-                                if (kStats) ++st.visits;
-                                uint32_t sk;
-                                const uint32_t nx = oct_step<kBofs>(sc, a, 0u, ray, kMaxDist, sk);
-                                if (nx == a.nNodes) {
-                                    sky = true;
-                                    state = kIdle;
-                                    cur = kNotWalking;
-                                    if (a.hitIds && last_frame) {
-                                        a.hitIds[(uint32_t)g64] = -1;
-                                        a.hitT[(uint32_t)g64] = kMaxDist;
-                                    }
-                                } else {
-                                    cur = nx;
-                                    leaf_i = sk;
-                                }
-                            }
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
                             if (a.hitIds && last_frame) {
@@ -1217,23 +1092,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         }
                     }
                 }
-#if RT_STEAL
-                if (kGoctTiles) {
-                    // this round's primary misses into the tile's word: bit (used + rank) per lane
-                    unsigned long long b = sky ? 1ull << (used + rank) : 0ull;
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off, 64);
-                    tile_sky |= b;
-                    if (used + take >= 64u) {  // the tile's last work item handed out
-                        if (lane == 0)
-                            reinterpret_cast<unsigned long long*>(a.frameFlags)[(size_t)slot * a.nTiles + tile] = tile_sky;
-                        tile_sky = 0ull;
-                    }
-                }
                 tile_used += take;
-#else
-                chunk_used += take;
-#endif
             }
         }
         uint64_t tB = kStats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1250,22 +1109,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         // wave priority by phase: traversal steps (short dependent LDS/VALU chains) issue ahead
         // of waves that shade or refill (long independent VALU runs), which fill the gaps
         // (profiles/r01/phase_priority_ab.txt)
-        if (kLdsScene || RT_GPHASE) __builtin_amdgcn_s_setprio(3);
+        __builtin_amdgcn_s_setprio(3);
         // Each step is wave-uniform: either a node step (TRAV lanes visit one node) or a
         // triangle step (LEAF lanes test one triangle), chosen by which serves more lanes per
         // instruction (weights ~ the two bodies' VALU cost), so the wave never pays both
         // bodies for a mix of lanes.
         for (;;) {
             uint32_t n_trav, n_leaf;
-            if (kSpec && a.specWalk) {
-                // walk at END with no leaf pending: the reference's traversal is over
-                if (cur == a.nNodes && pend < kLeafMin) {
-                    state = kShade;
-                    cur = kNotWalking;
-                }
-                n_trav = popc_ballot(cur < a.nNodes);  // (END lanes only wait for their triangles)
-                n_leaf = popc_ballot(pend >= kLeafMin);
-            } else if (kLdsScene) {
+            if (kLdsScene) {
                 // a walk parked on the END sentinel has finished the reference's traversal
                 // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
                 if (cur == a.nNodes) {
@@ -1279,13 +1130,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 n_leaf = popc_ballot(state == kLeaf);
             }
             if (n_trav + n_leaf == 0u) break;
-            {
-                const uint32_t n_shade = popc_ballot(state == kShade);
-                if (n_shade >= kShadeMin) break;
-                // few lanes left walking while many wait to shade: their traversal steps would
-                // run nearly empty, so shade the waiting batch now (RT_TRAV_LOW 0: off)
-                if (RT_TRAV_LOW > 0 && n_trav + n_leaf <= RT_TRAV_LOW && n_shade >= RT_SHADE_LOW) break;
-            }
+            if (popc_ballot(state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
             if (kStats) {
@@ -1302,41 +1147,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
             constexpr int kNodeBurst = kGlobalOct ? RT_ONODE_BURST : kLdsScene ? RT_NODE_BURST : RT_GNODE_BURST;
             constexpr int kTriBurst = kGlobalOct ? RT_OTRI_BURST : kLdsScene ? RT_TRI_BURST : RT_GTRI_BURST;
-            if (kSpec && a.specWalk && !leaf_step) {
-                // (t does not change during node steps: quieted once, not at every visit's min)
-                const float tq = __builtin_canonicalizef(h.t);
-#pragma unroll
-                for (int rep = 0; rep < kNodeBurst; ++rep) {
-                    if (cur < kLeafMin) {  // walking (END: the sentinel, always missed)
-                        if (kStats && cur != a.nNodes) ++st.visits;
-                        uint32_t hn, mn;
-                        const bool hit = oct_probe<kBofs>(sc, a, cur, ray, tq, hn, mn);
-                        // a passed leaf with none pending becomes the pending one (walk on at its
-                        // skip pointer); a second one stops the walk: cur = its code, leaf_i = it.
-                        // The successor on a hit is chosen from the record and `pend` alone, so
-                        // the box test's result feeds one select, as in the plain walk (the walk
-                        // is a dependent chain: latency, not issue, is its cost)
-                        const bool leaf_free = hn >= kLeafMin && pend < kLeafMin;
-                        const uint32_t on_hit = leaf_free ? mn : hn;
-                        leaf_i = cur;
-                        pend = hit && leaf_free ? hn : pend;
-                        cur = hit ? on_hit : mn;
-                    }
-                }
-            } else if (kSpec && a.specWalk) {
-#pragma unroll
-                for (int rep = 0; rep < kTriBurst; ++rep) {
-                    if (pend >= kLeafMin) {
-                        if (kStats) ++st.tests;
-                        const uint32_t idx = pend & 0x00ffffffu;
-                        ray_triangle<M, RT_KEEP_UV>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                        pend += 1u - kLeafMin;
-                        // leaf done and the walk stopped at a second one: re-visit that node at
-                        // the new t
-                        if (pend < kLeafMin && cur >= kLeafMin) cur = leaf_i;
-                    }
-                }
-            } else if (!leaf_step) {
+            if (!leaf_step) {
 #pragma unroll
                 for (int rep = 0; rep < kNodeBurst; ++rep) {
                     if (kLdsScene) {
@@ -1369,13 +1180,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if ((int32_t)cur >= (int32_t)kLeafMin) {
                             if (kStats) ++st.tests;
                             const uint32_t idx = cur & 0x00ffffffu;
-                            ray_triangle<M, RT_KEEP_UV>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
+                            ray_triangle<M>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
                             cur += 1u - kLeafMin;
                             if (cur < kLeafMin) cur = leaf_i;
                         }
                     } else if (state == kLeaf) {
                         if (kStats) ++st.tests;
-                        ray_triangle<M, RT_KEEP_UV>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
+                        ray_triangle<M>(sc.tris + 3 * (size_t)leaf_i, (int32_t)leaf_i, ray, h);
                         ++leaf_i;
                         if (leaf_i == leaf_end) state = cur == kEnd ? kShade : kTrav;
                     }
@@ -1384,8 +1195,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         }
 
         // ---- shading ---------------------------------------------------------------------------
-        if (kLdsScene) __builtin_amdgcn_s_setprio(RT_PRIO_SHADE);
-        else if (RT_GPHASE) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(RT_PRIO_SHADE);
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
         if (kStats) {
             cyc_trav += tC - tB;
@@ -1403,7 +1213,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     a.hitT[gid - (fused ? last : 0u)] = h.t;
                 }
             }
-            const bool more = shade_bounce<M, kStats>(RT_KEEP_UV ? h : with_uv<M>(sc, h, ray), ray, radiance, beta, seed, sc, a, st);
+            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
             ++bounce;
             if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
@@ -1472,16 +1282,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 // + 0, 0) in every component of every frame (kernel_bvh.cl:358-362, :383); if it also held
 // K_old, its result is one per-launch constant K_out = chain(K_old; K_rad x nFrames), computed
 // once by accum_key (one lane, same policy and operations).  Those pixels are written
-// directly; the others are accumulated in place (one 8x8 tile per wave), or -- several tiles
-// per wave (RT_ACCUM_TPW) -- through a per-wave LDS queue 64 at a time.  The key never
-// affects results, only how often the shortcut applies: K_old chains from the previous
-// launch's K_out (the value all-sky pixels then hold).
+// directly; the others are accumulated in place, one 8x8 tile per wave (a per-wave LDS queue of
+// several tiles' non-sky pixels, 64 at a time, measured no faster and was removed in round 5).
+// The key never affects results, only how often the shortcut applies: K_old chains from the
+// previous launch's K_out (the value all-sky pixels then hold).
 // Key words: [0] valid, [1] K_rad bits, [2] K_old, [3] K_out.
-// the frame radiances of one pixel, all loads issued together (no dependent round trips); a
-// flagged frame (frameFlags: radiance (K_rad, K_rad, K_rad), not stored) reads as K_rad
-struct FrameRad {
-    float4 r[kMaxFusedFrames];
-};
+// a pixel's frame flags (flagTiles 0: a byte per frame and work item)
 __device__ __forceinline__ uint32_t load_flags(const KernelArgs& a, uint32_t gid) {
     uint32_t fl = 0;
 #pragma unroll
@@ -1497,34 +1303,12 @@ __device__ __forceinline__ uint32_t load_tile_flags(const KernelArgs& a, uint32_
     for (uint32_t s = 0; s < a.nFrames; ++s) fl |= (uint32_t)((w[(size_t)s * a.nTiles] >> lane) & 1ull) << s;
     return fl;
 }
-__device__ __forceinline__ FrameRad load_frames(const KernelArgs& a, uint32_t gid, uint32_t flags, float krad) {
-    FrameRad f;
-#pragma unroll
-    for (uint32_t s = 0; s < kMaxFusedFrames; ++s)
-        f.r[s] = (s < a.nFrames && !((flags >> s) & 1u)) ? rad_load(a.radBuf + (size_t)s * a.radStride + gid)
-                                                          : make_float4(krad, krad, krad, 0.0f);
-    return f;
-}
-
-// The frame loop is NOT unrolled: one gamma step is ~6 ocml pow of ~120 instructions each, and
-// the unrolled 8-frame chain (twice, with the tail flush) made a 17k-instruction kernel whose
-// waves missed the instruction cache.  The frames stay loaded up front and rotate through r[0].
-template <class M>
-__device__ __forceinline__ F3 accum_chain(const KernelArgs& a, F3 v, FrameRad f) {
-#pragma unroll 1
-    for (uint32_t s = 0; s < a.nFrames; ++s) {
-        v = gamma_out<M>(a.frameCount + s, v, F3{f.r[0].x, f.r[0].y, f.r[0].z});
-#pragma unroll
-        for (uint32_t k = 0; k + 1 < kMaxFusedFrames; ++k) f.r[k] = f.r[k + 1];
-    }
-    return v;
-}
-
-// The same chain with each frame's radiance loaded when its step runs: few registers, so the
-// accumulation waves fit beside a running render grid (RT_ACCUM_VGPRS, co-resident overlap;
-// rt_capi.cpp).  Same values, same operations, same order.
-// gamma_out with its six pow evaluated one after another (scheduling barriers between them): the
-// same operations and bits, at a third of the interleaved form's live registers
+// The gamma chain of a pixel's frames (kernel_bvh.cl:449-455 per frame, in order), each frame's
+// radiance loaded when its step runs, the six pow of a step one after another (scheduling
+// barriers between them): few registers, so the accumulation waves fit beside a running render
+// grid (co-resident overlap, rt_capi.cpp).  Same values, same operations, same order.  The loop
+// is not unrolled: a gamma step is ~6 ocml pow of ~120 instructions each, and an unrolled 8-frame
+// chain made a 17k-instruction kernel whose waves missed the instruction cache.
 template <class M>
 __device__ __forceinline__ F3 gamma_out_serial(uint32_t frameCount, F3 old, F3 rad) {
     if (frameCount == 0) {
@@ -1564,10 +1348,8 @@ __device__ __forceinline__ F3 accum_chain_lean(const KernelArgs& a, F3 v, uint32
 // radiance: the sky shortcut's frame flags are read back from the frames themselves, all set only
 // when every frame holds K_rad (a pixel whose old value is not K_old never asks; the first frame
 // that is not K_rad ends the scan).  The chain would read the same bits, so the flags change which
-// path writes K_out, never a value.  A/B: -DRT_NOFLAG_SKYSCAN=0.
-#ifndef RT_NOFLAG_SKYSCAN
-#define RT_NOFLAG_SKYSCAN 1
-#endif
+// path writes K_out, never a value (1.364 vs 1.357 ms/frame on the bunny proxy without the scan,
+// profiles/r04/noflag_skyscan_ab.txt).
 __device__ __forceinline__ uint32_t scan_sky_frames(const KernelArgs& a, uint32_t gid, float krad) {
     const uint32_t k = __float_as_uint(krad);
 #pragma unroll 1
@@ -1597,106 +1379,38 @@ __device__ __forceinline__ void accum_key_body(const KernelArgs& a, uint32_t* ke
     key[0] = 1u;
 }
 
-// accumulation launch occupancy (A/B builds: -DRT_ACCUM_WAVES=n, -DRT_ACCUM_VGPRS=n)
-#ifndef RT_ACCUM_VGPRS
-#define RT_ACCUM_VGPRS 32
-#endif
-#ifdef RT_ACCUM_WAVES
-#define RT_ACCUM_OCC __attribute__((amdgpu_waves_per_eu(RT_ACCUM_WAVES, 8)))
-#elif RT_ACCUM_VGPRS
 // a register cap that fits one accumulation wave per SIMD beside the render grid (5 waves of
 // 96 VGPRs on the LDS path, 6 of 80 on the global path: 32 of 512 left)
-#define RT_ACCUM_OCC __attribute__((amdgpu_num_vgpr(RT_ACCUM_VGPRS)))
-#else
-#define RT_ACCUM_OCC
-#endif
-#ifndef RT_ACCUM_TPW
-#define RT_ACCUM_TPW 1
-#endif
-constexpr uint32_t kAccumTilesPerWave = RT_ACCUM_TPW;  // 8x8 tiles per wave of the accumulation launch
-#ifndef RT_ACCUM_WG_WAVES
-#define RT_ACCUM_WG_WAVES 4
-#endif
-constexpr uint32_t kAccumWgWaves = RT_ACCUM_WG_WAVES;  // waves per accumulation workgroup
-constexpr uint32_t kAccumQueue = 128;        // per-wave queue of non-sky pixels (gid)
+#define RT_ACCUM_OCC __attribute__((amdgpu_num_vgpr(32)))
+constexpr uint32_t kAccumWgWaves = 4;  // waves per accumulation workgroup, one 8x8 tile each
 
-#ifndef RT_ACCUM_PRIO
-#define RT_ACCUM_PRIO 0  // wave priority of the accumulation launch (0: below the render's)
-#endif
 template <class M>
 __device__ __forceinline__ void accum_frames_body(const KernelArgs& a, const uint32_t* key) {
-    if (RT_ACCUM_PRIO > 0) __builtin_amdgcn_s_setprio(RT_ACCUM_PRIO);
-    // per wave: queued pixels as {tile of the wave t << 16 | frame flags << 8 | lane in the tile}
-    // (the chain needs the pixel's work-item id and its flags: both re-formed from one word)
-    __shared__ uint32_t queue[kAccumWgWaves][kAccumQueue];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t* q = queue[wv];
-    uint32_t qn = 0;  // wave-uniform
     const uint32_t kold = key[2], kout = key[3];
     const float krf = __uint_as_float(key[1]);
-    const uint32_t tile0 = (blockIdx.x * kAccumWgWaves + wv) * kAccumTilesPerWave;
-    for (uint32_t t = 0; t < kAccumTilesPerWave; ++t) {
-        const uint32_t tile = tile0 + t;
-        if (tile >= a.nTiles) break;  // wave-uniform
-        const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-        const uint32_t x = tx * 8u + (lane & 7u), row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (lane >> 3);
-        const uint64_t g64 = (uint64_t)row * a.width + x;
-        const bool live = x < a.width && row < a.rowBegin + a.rowCount && g64 >= a.gidBegin && g64 < a.gidEnd;
-        const uint32_t gid = (uint32_t)g64;
-        bool sky = false;
-        uint32_t fl = 0;
-        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (live) {
-            if (a.frameCount != 0u) o = a.result[gid];
-            const bool old_sky = a.frameCount == 0u ||
-                                 (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold);
-            fl = a.flagTiles == 1u ? load_tile_flags(a, tile, lane)
-                 : a.flagTiles == 2u ? (RT_NOFLAG_SKYSCAN && old_sky ? scan_sky_frames(a, gid, krf) : 0u)
-                                     : load_flags(a, gid);
-            sky = fl == (1u << a.nFrames) - 1u && old_sky;
-            if (sky) {
-                const float v = __uint_as_float(kout);
-                a.result[gid] = make_float4(v, v, v, 0.0f);
-            }
-        }
-        const bool push = live && !sky;
-        if (kAccumTilesPerWave == 1u) {
-            // one tile per wave: the non-sky pixels accumulate in place (a queue would only move
-            // them to the low lanes of the same single round)
-            if (push) {
-#if RT_ACCUM_VGPRS
-                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, gid, fl, krf);
-#else
-                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, gid, fl, krf));
-#endif
-                a.result[gid] = make_float4(v.x, v.y, v.z, 0.0f);
-            }
-            continue;
-        }
-        const unsigned long long m = __ballot(push);
-        if (push) q[qn + lane_rank(m)] = t << 16 | fl << 8 | lane;
-        qn += (uint32_t)__popcll(m);
-        const bool last = t + 1 == kAccumTilesPerWave || tile + 1 >= a.nTiles;
-        // accumulate up to 64 queued pixels, one per lane; after the wave's last tile, until empty
-        // (one call site: the chain is the bulk of the kernel's code)
-        while (qn >= 64u || (last && qn > 0u)) {
-            if (lane < qn) {
-                const uint32_t e = q[lane], pl = e & 63u, gfl = (e >> 8) & 0xffu;
-                const uint32_t qt = tile0 + (e >> 16), qy = qt / a.tilesX;
-                const uint32_t g = (a.rowBegin + (qy * a.bandPeriod + a.bandPhase) * 8u + (pl >> 3)) * a.width +
-                                   (qt - qy * a.tilesX) * 8u + (pl & 7u);
-                const float4 o = a.frameCount != 0u ? a.result[g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#if RT_ACCUM_VGPRS
-                const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, g, gfl, krf);
-#else
-                const F3 v = accum_chain<M>(a, F3{o.x, o.y, o.z}, load_frames(a, g, gfl, krf));
-#endif
-                a.result[g] = make_float4(v.x, v.y, v.z, 0.0f);
-            }
-            qn = qn >= 64u ? qn - 64u : 0u;
-            if (lane < qn) q[lane] = q[64u + lane];
-        }
+    const uint32_t tile = blockIdx.x * kAccumWgWaves + wv;
+    if (tile >= a.nTiles) return;  // wave-uniform
+    const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
+    const uint32_t x = tx * 8u + (lane & 7u), row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (lane >> 3);
+    const uint64_t g64 = (uint64_t)row * a.width + x;
+    const bool live = x < a.width && row < a.rowBegin + a.rowCount && g64 >= a.gidBegin && g64 < a.gidEnd;
+    if (!live) return;
+    const uint32_t gid = (uint32_t)g64;
+    float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (a.frameCount != 0u) o = a.result[gid];
+    const bool old_sky = a.frameCount == 0u ||
+                         (__float_as_uint(o.x) == kold && __float_as_uint(o.y) == kold && __float_as_uint(o.z) == kold);
+    const uint32_t fl = a.flagTiles == 1u ? load_tile_flags(a, tile, lane)
+                        : a.flagTiles == 2u ? (old_sky ? scan_sky_frames(a, gid, krf) : 0u)
+                                            : load_flags(a, gid);
+    if (fl == (1u << a.nFrames) - 1u && old_sky) {
+        const float v = __uint_as_float(kout);
+        a.result[gid] = make_float4(v, v, v, 0.0f);
+        return;
     }
+    const F3 v = accum_chain_lean<M>(a, F3{o.x, o.y, o.z}, gid, fl, krf);
+    a.result[gid] = make_float4(v.x, v.y, v.z, 0.0f);
 }
 
 // One packed material record (pack_mats, once per bound scene): the material fields plus the

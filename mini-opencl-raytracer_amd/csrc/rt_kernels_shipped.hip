@@ -59,7 +59,7 @@ __global__ void accum_key_shipped(KernelArgs a, uint32_t* key) {
 }
 
 hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipStream_t st) {
-    const dim3 grid((a.nTiles + kAccumWgWaves * kAccumTilesPerWave - 1u) / (kAccumWgWaves * kAccumTilesPerWave));
+    const dim3 grid((a.nTiles + kAccumWgWaves - 1u) / kAccumWgWaves);
     hipLaunchKernelGGL(accum_key_shipped, dim3(1), dim3(64), 0, st, a, key);
     hipLaunchKernelGGL(accum_frames_shipped, grid, dim3(64 * kAccumWgWaves), 0, st, a, key);
     return hipGetLastError();

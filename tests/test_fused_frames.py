@@ -95,7 +95,7 @@ def test_fused_sky_shortcut_chain(cornell, force_global):
     a math-mode switch and a restart at frame 1 over a non-sky history: every call's output equals
     the per-frame launches (16:9 view: about half of the pixels see only sky).  force_global: the
     octant walk over HBM/L2, whose radiance sets carry no flags -- the accumulation reads a pixel's
-    all-sky frames back from the radiance itself (RT_NOFLAG_SKYSCAN)."""
+    all-sky frames back from the radiance itself."""
     W, H = 320, 180
     seq = [(1, 4, 1.0, N.MATH_SHIPPED), (5, 4, 1.0, N.MATH_SHIPPED), (1, 8, 1.0, N.MATH_SHIPPED),
            (1, 3, 0.6, N.MATH_SHIPPED), (4, 2, 0.6, N.MATH_DEVICELIB), (0, 2, 2.0, N.MATH_PINNED),
