@@ -270,7 +270,10 @@ constexpr uint32_t kLeafMin = 1u << 24;
 // even -- an odd plane stride (x 16 B) staggers the eight planes over the LDS banks, so lanes of
 // different octants at the same node do not collide (an even stride of 40 put planes o and o+2
 // on the same banks: +40 % bank-conflict cycles)
-inline uint32_t oct_stride(uint32_t n) { return (n + 1) | 1u; }
+#ifndef RT_OCT_STRIDE_MIN
+#define RT_OCT_STRIDE_MIN 0  // diagnostic A/B builds: the least octant-plane stride (LDS bank-conflict sensitivity)
+#endif
+inline uint32_t oct_stride(uint32_t n) { return std::max<uint32_t>((n + 1) | 1u, RT_OCT_STRIDE_MIN); }
 // float4 offset of the B planes: rtk::kOctB for trees of at most kOctBMaxStride records per plane
 // (a node step then reads B at an immediate offset from A), else right after the A planes
 inline uint32_t oct_b(uint32_t n) {
