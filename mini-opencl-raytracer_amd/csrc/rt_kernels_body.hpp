@@ -899,7 +899,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     uint64_t rt_dry = 0;  // when this wave found the work counter dry
 #endif
     // diagnostic lane-utilisation counters (wave-uniform): steps / rounds and lanes served
-    uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
+    [[maybe_unused]] uint64_t u_nsteps = 0, u_nlanes = 0, u_tsteps = 0, u_tlanes = 0, u_srounds = 0, u_slanes = 0,
              u_rrounds = 0, u_rlanes = 0, u_other = 0, u_shadew = 0, u_freew = 0, u_pad = 0;
     // RT_LDS_CONFLICTS: modelled (ideal, actual) LDS cycles per read site -- [0,1] a node visit's A
     // read (its B read has the same addresses + a constant: the same cycles), [2..5] the A read if
