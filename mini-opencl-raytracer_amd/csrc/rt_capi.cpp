@@ -1078,7 +1078,11 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
     // (48 B per triangle, 64 B per material); no stack
-    const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
+#ifndef RT_SHADE_GLOBAL
+#define RT_SHADE_GLOBAL 0  // (rt_kernels_body.hpp: shading records read in place)
+#endif
+    const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * (RT_SHADE_GLOBAL ? 48 : 96) +
+                               (RT_SHADE_GLOBAL ? 0 : (size_t)k->n_mats * 64);
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
 
     // scenes too large for LDS: the step schedule may walk the octant records in HBM/L2

@@ -134,6 +134,13 @@ constexpr uint32_t kLeafMin = 1u << 24;
 // Scene into LDS once per workgroup (when it fits), else read in place.  kGlobalOct: the octant
 // records, triangles and shading records of a scene too large for LDS, read from HBM/L2 by the
 // LDS path's walk (same record formats, nothing staged).
+// A/B: the shading and material records of an LDS scene read in place (L1/L2) instead of from
+// LDS: 4 KB less LDS per Cornell workgroup (30.3 -> 26.2 KB, so 6 workgroups fit a CU's LDS
+// where 5 of 96-VGPR waves fit its registers: the next launch's workgroups can start beside a
+// draining one)
+#ifndef RT_SHADE_GLOBAL
+#define RT_SHADE_GLOBAL 0
+#endif
 template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -142,6 +149,12 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
         const int tid = threadIdx.x;
         float4* lo = smem;
         float4* lt = lo + a.octRecords;
+        if (RT_SHADE_GLOBAL) {
+            for (uint32_t i = tid; i < a.octRecords; i += 256) lo[i] = a.octNodes[i];
+            for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+            __syncthreads();
+            return SceneView{nullptr, lt, lo, a.shadeTris, a.shadeMats};
+        }
         float4* ls = lt + 3 * a.nTris;
         float4* lm = ls + 3 * a.nTris;
         for (uint32_t i = tid; i < a.octRecords; i += 256) lo[i] = a.octNodes[i];
@@ -161,7 +174,8 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kGlobalOct ? 0u : kLdsScene ? a.octRecords + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
+    return kGlobalOct ? 0u : kLdsScene ? a.octRecords + (RT_SHADE_GLOBAL ? 3u : 6u) * a.nTris + (RT_SHADE_GLOBAL ? 0u : 4u * a.nMats)
+                                       : 4u * a.nTop;
 }
 
 struct Traversal {
