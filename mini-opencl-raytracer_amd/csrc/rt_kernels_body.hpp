@@ -616,6 +616,9 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
 // streamed past the caches (nontemporal) where the render reads its scene through them (HBM/L2
 // scene path: bunny proxy 1.425 -> 1.404 ms/frame, profiles/r02/nt_rad_ab.txt; the LDS path
 // showed no gain for its stores)
+#ifndef RT_GOCT_NT
+#define RT_GOCT_NT 1  // A/B: 0 = plain stores on the scene-in-HBM paths too
+#endif
 typedef float rad_v4f __attribute__((ext_vector_type(4)));
 template <bool kNt>
 __device__ __forceinline__ void rad_store(float4* p, float x, float y, float z) {
@@ -941,7 +944,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     // (ray ring: the tile's flags were written when it was generated -- a
                     // path that still ends as K_rad stores its radiance like any other, which
                     // the accumulation reads to the same bits)
-                    if (!skyv || kRing || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
+                    if (!skyv || kRing || kNoFlags) rad_store<(!kLdsScene || kGlobalOct) && RT_GOCT_NT>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
                     if (!kRing && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
