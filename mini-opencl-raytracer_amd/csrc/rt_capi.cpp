@@ -1105,7 +1105,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
+                 (si == RT_SCHED_STEP && lds ? 4 * rtk::ring_wave_bytes(fused) : 0) +
                  (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring

@@ -833,7 +833,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         constexpr bool kRingLds = kLdsScene && !kGlobalOct;
         steal = reinterpret_cast<unsigned long long*>(
             smem_s + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
-            (kRingLds ? 4u * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u) : 0u));
+            (kRingLds ? 4u * ring_wave_f4(fused) : 0u));
         if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
     }
     const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
@@ -878,9 +878,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // fused launches also keep {invDir, sign bits} (InitRay's tail, formed at fill) per slot;
     // per-frame launches re-form it at the pop (their finish queue leaves no LDS for it)
     float4* ring_d = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
-                     (uint32_t)(tid >> 6) * ((fused ? kRingWaveBytes : kRingWaveBytesPf) / 16u);
+                     (uint32_t)(tid >> 6) * ring_wave_f4(fused);
     float4* ring_i = ring_d + kRingSlots;
-    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (fused ? 2u : 1u) * kRingSlots);
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (ring_inv(fused) ? 2u : 1u) * kRingSlots);
     uint32_t rc_head = 0, rc_n = 0;  // wave-uniform: ring entries [rc_head, rc_head + rc_n)
     bool dry = false;                // wave-uniform: the work counter is exhausted
 
@@ -1059,7 +1059,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (keep) {
                         const uint32_t pos = lane_rank(vm);
                         ring_d[pos] = make_float4(cr.d.x, cr.d.y, cr.d.z, __uint_as_float(sd));
-                        if (fused) ring_i[pos] = make_float4(cr.inv.x, cr.inv.y, cr.inv.z, __uint_as_float(cr.sgn));
+                        if (ring_inv(fused)) ring_i[pos] = make_float4(cr.inv.x, cr.inv.y, cr.inv.z, __uint_as_float(cr.sgn));
                         ring_g[pos] = (uint32_t)g64 + (fused ? slot * a.radStride : 0u);
                     }
                     rc_head = 0;
@@ -1072,7 +1072,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     const float4 e = ring_d[rc_head + rank];
                     gid = ring_g[rc_head + rank];
                     seed = __float_as_uint(e.w);
-                    if (fused) {
+                    if (ring_inv(fused)) {
                         const float4 iv = ring_i[rc_head + rank];
                         ray.o = camPos;
                         ray.d = F3{e.x, e.y, e.z};
