@@ -270,10 +270,7 @@ constexpr uint32_t kLeafMin = 1u << 24;
 // even -- an odd plane stride (x 16 B) staggers the eight planes over the LDS banks, so lanes of
 // different octants at the same node do not collide (an even stride of 40 put planes o and o+2
 // on the same banks: +40 % bank-conflict cycles)
-#ifndef RT_OCT_STRIDE_MIN
-#define RT_OCT_STRIDE_MIN 0  // diagnostic A/B builds: the least octant-plane stride (LDS bank-conflict sensitivity)
-#endif
-inline uint32_t oct_stride(uint32_t n) { return std::max<uint32_t>((n + 1) | 1u, RT_OCT_STRIDE_MIN); }
+inline uint32_t oct_stride(uint32_t n) { return (n + 1) | 1u; }
 // float4 offset of the B planes: rtk::kOctB for trees of at most kOctBMaxStride records per plane
 // (a node step then reads B at an immediate offset from A), else right after the A planes
 inline uint32_t oct_b(uint32_t n) {
@@ -1078,11 +1075,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     // LDS: octant node records (8 x 32 B per node), triangles (48 B), shading records
     // (48 B per triangle, 64 B per material); no stack
-#ifndef RT_SHADE_GLOBAL
-#define RT_SHADE_GLOBAL 0  // (rt_kernels_body.hpp: shading records read in place)
-#endif
-    const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * (RT_SHADE_GLOBAL ? 48 : 96) +
-                               (RT_SHADE_GLOBAL ? 0 : (size_t)k->n_mats * 64);
+    const size_t scene_bytes = (size_t)oct_records(k->n_nodes) * 16 + (size_t)k->n_tris * 96 + (size_t)k->n_mats * 64;
     const bool lds = !k->force_global && k->oct_ok && scene_bytes <= kLdsBudget;
 
     // scenes too large for LDS: the step schedule may walk the octant records in HBM/L2
@@ -1105,7 +1098,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
                  (rtk::kWfExtendThreads / 64) * rtk::kWfRingBytes
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
-                 (si == RT_SCHED_STEP && lds ? 4 * rtk::ring_wave_bytes(fused) : 0) +
+                 (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
                  (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring

@@ -75,12 +75,6 @@ constexpr uint32_t kFinishWaveBytes = 64u * 16u;
 constexpr uint32_t kRingSlots = 64;
 constexpr uint32_t kRingWaveBytes = kRingSlots * 32u + kRingSlots * 4u;
 constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // per-frame: no invDir
-#ifndef RT_RING_NOINV
-#define RT_RING_NOINV 0  // A/B: 1 = fused rings keep no invDir either (re-formed at the pop)
-#endif
-constexpr bool ring_inv(bool fused) { return fused && !RT_RING_NOINV; }
-constexpr uint32_t ring_wave_bytes(bool fused) { return ring_inv(fused) ? kRingWaveBytes : kRingWaveBytesPf; }
-constexpr uint32_t ring_wave_f4(bool fused) { return ring_inv(fused) ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u; }
 // step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
 // from which its siblings take single tiles once the work counter is dry
 constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)

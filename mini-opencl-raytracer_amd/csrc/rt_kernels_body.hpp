@@ -134,13 +134,6 @@ constexpr uint32_t kLeafMin = 1u << 24;
 // Scene into LDS once per workgroup (when it fits), else read in place.  kGlobalOct: the octant
 // records, triangles and shading records of a scene too large for LDS, read from HBM/L2 by the
 // LDS path's walk (same record formats, nothing staged).
-// A/B: the shading and material records of an LDS scene read in place (L1/L2) instead of from
-// LDS: 4 KB less LDS per Cornell workgroup (30.3 -> 26.2 KB, so 6 workgroups fit a CU's LDS
-// where 5 of 96-VGPR waves fit its registers: the next launch's workgroups can start beside a
-// draining one)
-#ifndef RT_SHADE_GLOBAL
-#define RT_SHADE_GLOBAL 0
-#endif
 template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -149,12 +142,6 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
         const int tid = threadIdx.x;
         float4* lo = smem;
         float4* lt = lo + a.octRecords;
-        if (RT_SHADE_GLOBAL) {
-            for (uint32_t i = tid; i < a.octRecords; i += 256) lo[i] = a.octNodes[i];
-            for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
-            __syncthreads();
-            return SceneView{nullptr, lt, lo, a.shadeTris, a.shadeMats};
-        }
         float4* ls = lt + 3 * a.nTris;
         float4* lm = ls + 3 * a.nTris;
         for (uint32_t i = tid; i < a.octRecords; i += 256) lo[i] = a.octNodes[i];
@@ -174,8 +161,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
-    return kGlobalOct ? 0u : kLdsScene ? a.octRecords + (RT_SHADE_GLOBAL ? 3u : 6u) * a.nTris + (RT_SHADE_GLOBAL ? 0u : 4u * a.nMats)
-                                       : 4u * a.nTop;
+    return kGlobalOct ? 0u : kLdsScene ? a.octRecords + 6u * a.nTris + 4u * a.nMats : 4u * a.nTop;
 }
 
 struct Traversal {
@@ -616,9 +602,6 @@ __global__ __launch_bounds__(256) void kernel_entry(KernelArgs a) {
 // streamed past the caches (nontemporal) where the render reads its scene through them (HBM/L2
 // scene path: bunny proxy 1.425 -> 1.404 ms/frame, profiles/r02/nt_rad_ab.txt; the LDS path
 // showed no gain for its stores)
-#ifndef RT_GOCT_NT
-#define RT_GOCT_NT 1  // A/B: 0 = plain stores on the scene-in-HBM paths too
-#endif
 typedef float rad_v4f __attribute__((ext_vector_type(4)));
 template <bool kNt>
 __device__ __forceinline__ void rad_store(float4* p, float x, float y, float z) {
@@ -833,7 +816,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         constexpr bool kRingLds = kLdsScene && !kGlobalOct;
         steal = reinterpret_cast<unsigned long long*>(
             smem_s + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
-            (kRingLds ? 4u * ring_wave_f4(fused) : 0u));
+            (kRingLds ? 4u * (fused ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u) : 0u));
         if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
     }
     const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
@@ -878,9 +861,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // fused launches also keep {invDir, sign bits} (InitRay's tail, formed at fill) per slot;
     // per-frame launches re-form it at the pop (their finish queue leaves no LDS for it)
     float4* ring_d = smem + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
-                     (uint32_t)(tid >> 6) * ring_wave_f4(fused);
+                     (uint32_t)(tid >> 6) * (fused ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u);
     float4* ring_i = ring_d + kRingSlots;
-    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (ring_inv(fused) ? 2u : 1u) * kRingSlots);
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(ring_d + (fused ? 2u : 1u) * kRingSlots);
     uint32_t rc_head = 0, rc_n = 0;  // wave-uniform: ring entries [rc_head, rc_head + rc_n)
     bool dry = false;                // wave-uniform: the work counter is exhausted
 
@@ -944,7 +927,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     // (ray ring: the tile's flags were written when it was generated -- a
                     // path that still ends as K_rad stores its radiance like any other, which
                     // the accumulation reads to the same bits)
-                    if (!skyv || kRing || kNoFlags) rad_store<(!kLdsScene || kGlobalOct) && RT_GOCT_NT>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
+                    if (!skyv || kRing || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
                     if (!kRing && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
                 }
@@ -1059,7 +1042,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (keep) {
                         const uint32_t pos = lane_rank(vm);
                         ring_d[pos] = make_float4(cr.d.x, cr.d.y, cr.d.z, __uint_as_float(sd));
-                        if (ring_inv(fused)) ring_i[pos] = make_float4(cr.inv.x, cr.inv.y, cr.inv.z, __uint_as_float(cr.sgn));
+                        if (fused) ring_i[pos] = make_float4(cr.inv.x, cr.inv.y, cr.inv.z, __uint_as_float(cr.sgn));
                         ring_g[pos] = (uint32_t)g64 + (fused ? slot * a.radStride : 0u);
                     }
                     rc_head = 0;
@@ -1072,7 +1055,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     const float4 e = ring_d[rc_head + rank];
                     gid = ring_g[rc_head + rank];
                     seed = __float_as_uint(e.w);
-                    if (ring_inv(fused)) {
+                    if (fused) {
                         const float4 iv = ring_i[rc_head + rank];
                         ray.o = camPos;
                         ray.d = F3{e.x, e.y, e.z};

@@ -30,7 +30,7 @@ u = s["sched"]
 raw = [u[k] for k in ("node_steps", "node_lanes", "tri_steps", "tri_lanes", "shade_rounds", "shade_lanes",
                       "refill_rounds", "refill_lanes", "other_lanes", "shade_wait", "free_wait", "reserved")]
 sites = [("node A read (octant planes, stride %d: current)" % 41, 0, 2),
-         ("node A read, stride 43", 2, 2), ("node A read, stride 47", 4, 2),
+         ("node A read, stride 43", 2, 2), ("node A read, stride 48", 4, 2),
          ("triangle 16-B reads (each of two)", 6, 2), ("triangle 4-B e2.z read (16-B stride: current)", 8, 2),
          ("triangle e2.z from a dense float array", 10, 2)]
 print(f"4K Cornell, {frames} fused frames, 9 bounces: node visits {s['node_visits']}, triangle tests {s['tri_tests']}")
