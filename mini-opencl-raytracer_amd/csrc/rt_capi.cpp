@@ -1099,8 +1099,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
                  (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
-                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0) +
-                 (RT_GOCT_STAGE && si == RT_SCHED_STEP && goct && fused ? 4 * rtk::kStageWaveBytes : 0);
+                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end

@@ -78,14 +78,6 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 // step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
 // from which its siblings take single tiles once the work counter is dry
 constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)
-// step schedule, fused octant walks over HBM/L2: per wave, the radiance of kStageTiles 8x8 tiles
-// staged in LDS (64 float4 each) and written out a whole tile at a time, plus one record per
-// stage slot {owner tile id, radiances staged, pixels of the tile, first radiance index}
-#ifndef RT_GOCT_STAGE
-#define RT_GOCT_STAGE 0  // A/B (round 5): writes 1.335 -> 1.053e6 KB per bunny launch, +0.9-1.8 % time
-#endif
-constexpr uint32_t kStageTiles = 4;
-constexpr uint32_t kStageWaveBytes = kStageTiles * (64u * 16u + 16u);
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address

@@ -615,25 +615,6 @@ __device__ __forceinline__ float4 rad_load(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// fused octant walks over HBM/L2: the calling wave's stage slots (after the work-stealing words)
-__device__ __forceinline__ float4* stage_slots(float4* smem, int tid) {
-    return smem + kStealBytes / 16u + __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6) * (kStageWaveBytes / 16u);
-}
-// ... and their records (uint4 {owner, staged, pixels, base}, after the slots)
-__device__ __forceinline__ uint4* stage_records(float4* smem, int tid) {
-    return reinterpret_cast<uint4*>(stage_slots(smem, tid) + kStageTiles * 64u);
-}
-constexpr uint32_t kNoOwner = 0xffffffffu;
-// writes out one stage slot -- the radiance of the tile's pixels staged so far (a nonzero w marks
-// one), pixel `lane` at radiance index base + (lane / 8) * width + lane % 8: whole rows of 8
-// pixels, 128-B lines -- and frees it
-__device__ __forceinline__ void stage_flush(const KernelArgs& a, const float4* slot, uint4* rec, uint32_t base,
-                                            uint32_t lane) {
-    const float4 v = slot[lane];
-    if (__float_as_uint(v.w) != 0u) rad_store<true>(a.radBuf + base + (lane >> 3) * a.width + (lane & 7u), v.x, v.y, v.z);
-    if (lane == 0u) rec->x = kNoOwner;
-}
-
 __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
                                            uint32_t& len, bool& tail) {
     uint32_t b = 0;
@@ -904,19 +885,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // (Per-tile flag words decided at refill measured 1 % slower there: the root visit at refill
     // costs load instructions outside the node bursts, profiles/r04/goct_flags.txt.)
     const bool kNoFlags = kGlobalOct && fused && a.flagTiles == 2u;
-    // ... and write it through a per-wave LDS stage: a path's radiance goes to its tile's slot
-    // (tile id and pixel in the `bounce` register's upper bits: bits 8-13 pixel, 14-31 the wave's
-    // tile sequence number), and a tile whose paths have all finished is written as whole rows of 8
-    // pixels (128-B lines) at once.  Stored straight from the lane, paths of one 64-B block finish
-    // at different times and the block leaves L2 in between: 3.9 M blocks per bunny launch went
-    // out as two 32-B halves (profiles/r05/bunny_store_kind_ab.txt).  A tile still open when its
-    // stage slot comes round again (kStageTiles tiles later) is written as far as it got, and its
-    // remaining paths store their radiance themselves.
-    const bool kStage = RT_GOCT_STAGE && kNoFlags;
-    // (the slot records live in LDS: as registers they spilled 57 VGPRs of the walk to scratch)
-    if constexpr (kGlobalOct)
-        if (kStage && lane < (int)kStageTiles) stage_records(smem, tid)[lane] = make_uint4(kNoOwner, 0u, 0u, 0u);
-    uint32_t sg_seq = 0;  // wave-uniform: tiles taken (the current tile's id: sg_seq - 1)
     // work: chunks of a.chunkPixels pixels (whole 8x8 tiles) from one global counter --
     // one returning atomic per chunk, so the counter stays far from its throughput limit
     uint32_t chunk_base = 0, chunk_len = 0;    // wave-uniform
@@ -951,7 +919,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             // finished paths: the gamma accumulation through the finish queue, or (fused
             // frames) the radiance into its frame slot
             if (fused) {
-                uint32_t sb = kNoOwner;  // the stage slot this lane's radiance went to
                 if (state == kDone) {
                     // a radiance of (K_rad, K_rad, K_rad) -- a primary miss -- is only flagged
                     const bool skyv = __float_as_uint(radiance.x) == __float_as_uint(krad) &&
@@ -960,40 +927,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     // (ray ring: the tile's flags were written when it was generated -- a
                     // path that still ends as K_rad stores its radiance like any other, which
                     // the accumulation reads to the same bits)
-                    bool direct = !skyv || kRing || kNoFlags;
-                    if constexpr (kGlobalOct) if (kStage) {
-                        // the slot still holds this path's tile iff the tile is one of the last
-                        // kStageTiles taken (a finished tile has no paths left to ask)
-                        const uint32_t id = bounce >> 14, b = id & (kStageTiles - 1u);
-                        if (((sg_seq - 1u - id) & 0x3ffffu) < kStageTiles) {
-                            stage_slots(smem, tid)[b * 64u + ((bounce >> 8) & 63u)] =
-                                make_float4(radiance.x, radiance.y, radiance.z, __uint_as_float(1u));
-                            sb = b;
-                            direct = false;
-                        }
-                    }
-                    if (kGlobalOct ? direct : !skyv || kRing || kNoFlags)
-                        rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
+                    if (!skyv || kRing || kNoFlags) rad_store<!kLdsScene || kGlobalOct>(a.radBuf + gid, radiance.x, radiance.y, radiance.z);
                     if (!kRing && !kNoFlags) a.frameFlags[gid] = skyv ? 1u : 0u;
                     state = kIdle;
-                }
-                if constexpr (kGlobalOct) if (kStage) {
-                    // count the staged radiances per slot touched (usually one or two); a tile
-                    // with all its pixels staged is written out
-                    unsigned long long m = __ballot(sb != kNoOwner);
-                    while (m != 0ull) {
-                        const uint32_t k = __builtin_amdgcn_readlane(sb, (int)__builtin_ctzll(m));
-                        const unsigned long long mk = __ballot(sb == k);
-                        m &= ~mk;
-                        uint4* rec = stage_records(smem, tid) + k;
-                        const uint4 r = *rec;  // (the same address on every lane)
-                        const uint32_t cnt = __builtin_amdgcn_readfirstlane(r.y) + (uint32_t)__popcll(mk);
-                        if (cnt == __builtin_amdgcn_readfirstlane(r.z))
-                            stage_flush(a, stage_slots(smem, tid) + k * 64u, rec, __builtin_amdgcn_readfirstlane(r.w),
-                                        (uint32_t)lane);
-                        else if (lane == 0)
-                            rec->y = cnt;
-                    }
                 }
             }
             if (!fused && a.pfKeyIn && state == kDone &&
@@ -1177,31 +1113,6 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     slot = tile / a.nTiles;
                     tile -= slot * a.nTiles;
                 }
-                if constexpr (kGlobalOct) if (kStage && used == 0u) {
-                    // a new tile: its stage slot (written out first if an older tile still holds
-                    // it), cleared; the number of its pixels and its first pixel's radiance index
-                    const uint32_t b = sg_seq & (kStageTiles - 1u);
-                    uint4* rec = stage_records(smem, tid) + b;
-                    const uint4 r = *rec;
-                    if (__builtin_amdgcn_readfirstlane(r.x) != kNoOwner)
-                        stage_flush(a, stage_slots(smem, tid) + b * 64u, rec, __builtin_amdgcn_readfirstlane(r.w),
-                                    (uint32_t)lane);
-                    reinterpret_cast<uint32_t*>(stage_slots(smem, tid) + b * 64u + (uint32_t)lane)[3] = 0u;
-                    const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                    const uint32_t row0 = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u;
-                    const uint64_t g0 = (uint64_t)row0 * a.width + tx * 8u;
-                    // pixels of the tile inside the image, the band and the work range (scalar)
-                    uint32_t need = 0u;
-                    const uint64_t nc = min(8u, a.width - min(a.width, tx * 8u));
-                    for (uint32_t r = 0; r < 8u && row0 + r < rowEnd; ++r) {
-                        const uint64_t g = g0 + (uint64_t)r * a.width;
-                        const uint64_t lo = max(g, a.gidBegin), hi = min(g + nc, a.gidEnd);
-                        need += hi > lo ? (uint32_t)(hi - lo) : 0u;
-                    }
-                    const uint32_t base = (uint32_t)g0 + slot * a.radStride;
-                    if (lane == 0) *rec = make_uint4(sg_seq & 0x3ffffu, 0u, need, base);
-                    ++sg_seq;
-                }
                 if (state == kIdle && rank < take) {
                     const uint32_t w = used + rank;  // chunks are whole 8x8 tiles
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
@@ -1216,7 +1127,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if (fused) gid += slot * a.radStride;
                         radiance = f3s(0.0f);
                         beta = f3s(1.0f);
-                        bounce = kStage ? (w << 8) | (((sg_seq - 1u) & 0x3ffffu) << 14) : 0u;  // (bits 0-7 count)
+                        bounce = 0;
                         if (bounces > 0u) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
@@ -1367,7 +1278,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
         }
         if (state == kShade) {
-            if ((kGlobalOct ? bounce & 0xffu : bounce) == 0u && a.hitIds) {  // primary hit outputs (extension); fused: last frame's
+            if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension); fused: last frame's
                 const uint32_t last = (a.nFrames - 1u) * a.radStride;
                 if (!fused || gid >= last) {
                     a.hitIds[gid - (fused ? last : 0u)] = h.prim;
@@ -1376,7 +1287,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
             const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
             ++bounce;
-            if (!more || (kGlobalOct ? bounce & 0xffu : bounce) >= bounces) {
+            if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
                 state = kDone;
                 if (kLdsScene) cur = kNotWalking;

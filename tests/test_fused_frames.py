@@ -226,11 +226,10 @@ def test_global_scene_walks(cornell, math, fused, goct):
 
 
 @pytest.mark.parametrize("case", ["whole", "bands", "work_range"])
-def test_octant_walk_staged_radiance_ragged(cornell, case):
-    """Fused octant walks over HBM/L2 stage each tile's radiance in LDS and write it out a tile at a
-    time (rt_kernels_body.hpp stage_flush): ragged edge tiles (250 x 139), band interleaves and work
-    ranges that start and end inside a tile, with tiles left open when their stage slot comes round
-    again -- the bits of per-frame launches."""
+def test_octant_walk_fused_ragged(cornell, case):
+    """Fused octant walks over HBM/L2 (every path stores its radiance, no flags) on ragged edge tiles
+    (250 x 139), band interleaves and work ranges that start and end inside a tile -- the bits of
+    per-frame launches."""
     W, H = 250, 139
     kw = {"whole": {}, "bands": {"interleave": (3, 2)}, "work_range": {"work_range": (1234, W * H - 4321)}}[case]
     _same(_render(cornell, W, H, 1, 6, True, force_global=True, tuning={"global_oct": 1}, **kw),
