@@ -270,6 +270,43 @@ __device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelAr
     return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
 }
 
+// Scenes read from HBM/L2 (the octant walk over global records): a node or triangle step's loads
+// are the work the vector-memory address unit is bound by (bunny proxy: `ta_busy` 0.91).  A step's
+// ~40 walking lanes read only ~5 distinct records (camera rays of a tile and its frames walk
+// together), and in 11 % of the steps all of them read the same one (profiles/r05/goct_coherence.txt):
+// such a step reads it once through the scalar cache (s_load, no address-unit work): bunny proxy
+// 1.357 -> 1.351 ms/frame, `TA_TA_BUSY` -5.4 % (profiles/r05/goct_scalar_ab.txt).  (The first active
+// lane's record through the scalar cache in every step, the other lanes' by vector loads, cut the
+// address unit's wavefronts by 10 % but put the scalar cache's latency on every step: +15 %.)
+typedef float sv4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const sv4f cv4f;
+typedef __attribute__((address_space(4))) const float cf32;
+
+template <bool kBofs>
+__device__ __forceinline__ uint32_t oct_step_g(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                               float t, uint32_t& skip) {
+    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+    const uint32_t ob = kBofs ? kOctB : a.octB;
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i);
+    const cv4f* cp = (const cv4f*)sc.onodes;
+    sv4f A, B;
+    if (__ballot(i != i0) == 0ull) {  // every walking lane at one record
+        A = cp[i0];
+        B = cp[i0 + ob];
+    } else {
+        A = *reinterpret_cast<const sv4f*>(sc.onodes + i);
+        B = *reinterpret_cast<const sv4f*>(sc.onodes + i + ob);
+    }
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    skip = __float_as_uint(B.w);
+    return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
+}
+
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
 // early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
 // ones the reference computes where it reaches them; the rest are discarded.  A wave
@@ -280,11 +317,7 @@ struct TriEval {
 };
 
 template <class M>
-__device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
-    // {p1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z}: two 16-B reads and one 4-B read (pack_tris)
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f a = *reinterpret_cast<const v4f*>(tri), b = *reinterpret_cast<const v4f*>(tri + 1);
-    const float c = *reinterpret_cast<const float*>(tri + 2);
+__device__ __forceinline__ TriEval tri_eval_v(sv4f a, sv4f b, float c, const Ray& r) {
     const F3 p1{a.x, a.y, a.z}, e1{a.w, b.x, b.y}, e2{b.z, b.w, c};
     const F3 pvec = M::cross(r.d, e2);
     const float det = M::dot(e1, pvec);
@@ -297,13 +330,38 @@ __device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
     return TriEval{det, u, v, t};
 }
 
+template <class M>
+__device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
+    // {p1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z}: two 16-B reads and one 4-B read (pack_tris)
+    return tri_eval_v<M>(*reinterpret_cast<const sv4f*>(tri), *reinterpret_cast<const sv4f*>(tri + 1),
+                         *reinterpret_cast<const float*>(tri + 2), r);
+}
+
+// the same on a scene read from HBM/L2 (oct_step_g): through the scalar cache when every testing
+// lane is at one triangle
+template <class M>
+__device__ __forceinline__ TriEval tri_eval_g(const float4* tris, uint32_t idx, const Ray& r) {
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(idx);
+    const cv4f* cp = (const cv4f*)tris;
+    sv4f va, vb;
+    float vc;
+    if (__ballot(idx != i0) == 0ull) {  // every testing lane at one triangle
+        va = cp[3u * i0];
+        vb = cp[3u * i0 + 1u];
+        vc = *((cf32*)(tris + 3u * i0 + 2u));
+    } else {
+        va = *reinterpret_cast<const sv4f*>(tris + 3u * idx);
+        vb = *reinterpret_cast<const sv4f*>(tris + 3u * idx + 1u);
+        vc = *reinterpret_cast<const float*>(tris + 3u * idx + 2u);
+    }
+    return tri_eval_v<M>(va, vb, vc, r);
+}
+
 // kUV = false: keep only {t, primitive} during the walk (two fewer live registers); the
 // barycentrics of the closest hit are re-evaluated at shading time (hit_uv) from the same
 // triangle and ray, which reproduces the accepted values bit for bit.
-template <class M, bool kUV = true>
-__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r,
-                                             Traversal& h) {
-    const TriEval e = tri_eval<M>(tri, r);
+template <bool kUV = true>
+__device__ __forceinline__ void tri_accept(const TriEval& e, int32_t idx, Traversal& h) {
     // The reference's early returns (det < 1e-8, u < 0, u > 1, v < 0, u + v > 1; then t <
     // isect.t) in VALU arithmetic rather than a chain of mask operations: for operands that are
     // not NaN, x < y <=> x - y < 0 exactly (an IEEE difference of distinct floats is never
@@ -323,6 +381,11 @@ __device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, con
             h.v = e.v;
         }
     }
+}
+
+template <class M, bool kUV = true>
+__device__ __forceinline__ void ray_triangle(const float4* tri, int32_t idx, const Ray& r, Traversal& h) {
+    tri_accept<kUV>(tri_eval<M>(tri, r), idx, h);
 }
 
 template <class M>
@@ -723,6 +786,17 @@ __device__ __forceinline__ uint32_t popc_ballot(bool p) { return (uint32_t)__pop
 #ifndef RT_LDS_CONFLICTS
 #define RT_LDS_CONFLICTS 0
 #endif
+// distinct keys among the active lanes (wave-uniform); the HBM/L2 walk's coherence counters
+__device__ __noinline__ uint32_t distinct_keys(bool act, uint32_t key) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const unsigned long long am = __ballot(act);
+    bool first = act;
+    for (uint32_t j = 0; j < 64u; ++j) {
+        const uint32_t kj = __shfl(key, (int)j, 64);
+        if (((am >> j) & 1ull) && j < lane && kj == key) first = false;
+    }
+    return (uint32_t)__popcll(__ballot(first));
+}
 __device__ __forceinline__ uint32_t lds_group(uint32_t l, bool b128) {
     if (!b128) return l >> 5;
     const uint32_t h = l & 31u;
@@ -1217,9 +1291,27 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             }
                         }
 #endif
+#if RT_LDS_CONFLICTS
+                        // HBM/L2 octant walk: per node step, active lanes, distinct records, distinct
+                        // 128-B lines, steps with one record ([0..3]); per triangle step [4..7]
+                        if (kStats && kGlobalOct) {
+                            const bool act = cur < kLeafMin;
+                            const uint32_t na = popc_ballot(act);
+                            if (na) {
+                                const uint32_t i = __umul24(ray.sgn, a.octStride) + cur;
+                                const uint32_t dk = distinct_keys(act, i);
+                                lm[0] += na;
+                                lm[1] += dk;
+                                lm[2] += distinct_keys(act, i >> 3);
+                                lm[3] += dk == 1u;
+                                lm[8] += 1u;
+                            }
+                        }
+#endif
                         if (cur < kLeafMin) {
                             if (kStats && cur != a.nNodes) ++st.visits;
-                            cur = oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
+                            cur = kGlobalOct ? oct_step_g<kBofs>(sc, a, cur, ray, h.t, leaf_i)
+                                             : oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
                         }
                     } else if (state == kTrav) {
                         if (kStats) ++st.visits;
@@ -1249,10 +1341,28 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                             lds_model(act, t4, z & 31u, false, lm[10], lm[11]);
                         }
 #endif
+#if RT_LDS_CONFLICTS
+                        if (kStats && kGlobalOct) {
+                            const bool act = (int32_t)cur >= (int32_t)kLeafMin;
+                            const uint32_t na = popc_ballot(act);
+                            if (na) {
+                                const uint32_t idx = cur & 0x00ffffffu;
+                                const uint32_t dk = distinct_keys(act, idx);
+                                lm[4] += na;
+                                lm[5] += dk;
+                                lm[6] += distinct_keys(act, (3u * idx) >> 3);
+                                lm[7] += dk == 1u;
+                                lm[9] += 1u;
+                            }
+                        }
+#endif
                         if ((int32_t)cur >= (int32_t)kLeafMin) {
                             if (kStats) ++st.tests;
                             const uint32_t idx = cur & 0x00ffffffu;
-                            ray_triangle<M>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
+                            if (kGlobalOct)
+                                tri_accept(tri_eval_g<M>(sc.tris, idx, ray), (int32_t)idx, h);
+                            else
+                                ray_triangle<M>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
                             cur += 1u - kLeafMin;
                             if (cur < kLeafMin) cur = leaf_i;
                         }
