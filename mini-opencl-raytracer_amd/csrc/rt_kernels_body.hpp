@@ -1293,7 +1293,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #endif
 #if RT_LDS_CONFLICTS
                         // HBM/L2 octant walk: per node step, active lanes, distinct records, distinct
-                        // 128-B lines, steps with one record ([0..3]); per triangle step [4..7]
+                        // 128-B lines, steps with one record ([0..3]), steps [8], with <= 2 and <= 4
+                        // records [10, 11]; per triangle step [4..7], steps [9]
                         if (kStats && kGlobalOct) {
                             const bool act = cur < kLeafMin;
                             const uint32_t na = popc_ballot(act);
@@ -1305,6 +1306,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                                 lm[2] += distinct_keys(act, i >> 3);
                                 lm[3] += dk == 1u;
                                 lm[8] += 1u;
+                                lm[10] += dk <= 2u;
+                                lm[11] += dk <= 4u;
                             }
                         }
 #endif

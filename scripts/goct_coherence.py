@@ -30,3 +30,4 @@ for name, o, steps in (("node steps", 0, raw[8]), ("triangle steps", 4, raw[9]))
     print(f"{name:15s} {steps:12d}: lanes/step {lanes / max(1, steps):5.1f}, distinct records/step "
           f"{rec / max(1, steps):5.1f}, distinct 128-B lines/step {lines / max(1, steps):5.1f}, "
           f"one-record steps {uni / max(1, steps):.3f}")
+print(f"node steps with <= 2 records {raw[10] / max(1, raw[8]):.3f}, <= 4 records {raw[11] / max(1, raw[8]):.3f}")
