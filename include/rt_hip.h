@@ -263,7 +263,12 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     wave >= 2.5 tail chunks)
  *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)
  *   TOP_NODES                         global path: top-of-tree nodes staged in LDS (0-1024, 384)
- *   TILE_MAJOR                        fused work order: -1 auto (default), 0 frame-major, 1 tile-major
+ *   TILE_MAJOR                        fused work order: -1 auto (default: scenes in HBM/L2 pixel-major
+ *                                     for 2, 4 or 8 frames, else tile-major for large launches and
+ *                                     frame-major for small ones; LDS scenes frame-major),
+ *                                     0 frame-major, 1 tile-major (a tile's frames back to back),
+ *                                     2 pixel-major (a pixel's frames side by side in a wave; 2, 4 or 8
+ *                                     frames on scenes in HBM/L2, otherwise tile-major)
  *   PERFRAME_SKY                      per-frame sky shortcut: 0 off, 1 large launches (default),
  *                                     2 always
  *   WF_REFILL_MIN                     wavefront extend: take queued rays once this many lanes

@@ -72,7 +72,7 @@ struct rt_kernel_s {
     uint32_t* work_counter = nullptr;  // persistent schedules' chunk counters: [4] per render stream
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
-    int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major
+    int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major, 2 pixel-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
     int pf_defer = 2;                  // per-frame step launches through radiance slots + accumulation
                                        // (0 never, 1 always, 2 while the previous one still runs)
@@ -1125,10 +1125,21 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // bulk chunks only when every resident wave gets at least two of them; a small frame
         // (512x512: ~40 pixels per wave) is handed out 64 pixels at a time
         const uint64_t tot = (uint64_t)a.nTiles * 64u * n_frames, waves = grid * 4u;
-        // tile-major order for large fused launches on the HBM/L2 scene path: coherent fetches
-        // (bunny proxy, N = 1: -1.4 %); with few items per wave (multi-GPU ranks) it bunches a
-        // costly tile's frames into the tail, so frame-major there (work_order_ab.txt)
-        a.tileMajor = n_frames > 1 && (k->tile_major == 1 || (k->tile_major < 0 && !lds && tot >= 4096u * waves)) ? 1u : 0u;
+        // fused work order (step_body) on the HBM/L2 scene path: pixel-major when F is a power of two
+        // -- a pixel's frames side by side in a wave, so a step's lanes read fewer records: bunny
+        // proxy 1.352 -> 1.282 ms/frame, emulated N = 8 rank 1.637 -> 1.535 ms
+        // (profiles/r05/pixel_major_ab.txt); else tile-major for large launches (a tile's frames back
+        // to back: -1.4 %, profiles/r01/work_order_ab.txt) and frame-major for small ones (tile-major
+        // bunches a costly tile's frames into the tail); LDS scenes frame-major (the ray ring)
+        const bool pow2 = n_frames == 2 || n_frames == 4 || n_frames == 8;
+        const bool big = !lds && tot >= 4096u * waves;
+        a.tileMajor = n_frames < 2 ? 0u
+                      : k->tile_major == 2 ? (!lds && pow2 ? 2u : 1u)
+                      : k->tile_major == 1 ? 1u
+                      : k->tile_major == 0 ? 0u
+                      : !lds && pow2       ? 2u
+                      : big                ? 1u
+                                           : 0u;
         // the bulk share stops where the tail would hold less than two bulk chunks per wave: a
         // bulk chunk (512 pixel-frames, ~0.25 ms of a wave's time at 4K) taken just before the
         // split otherwise outlasts the tail that should even the waves out -- small launches
@@ -1634,7 +1645,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
             break;
         case RT_TUNE_BULK_PERCENT: if (!in(0, 100)) return RT_INVALID_VALUE; k->bulk_percent = (uint32_t)value; break;
         case RT_TUNE_TOP_NODES: if (!in(0, 1024)) return RT_INVALID_VALUE; k->top_limit = (uint32_t)value; k->packed_nodes_gen = ~0ull; break;
-        case RT_TUNE_TILE_MAJOR: if (!in(-1, 1)) return RT_INVALID_VALUE; k->tile_major = value; break;
+        case RT_TUNE_TILE_MAJOR: if (!in(-1, 2)) return RT_INVALID_VALUE; k->tile_major = value; break;
         case RT_TUNE_MAX_BLOCKS: if (!in(0, 64)) return RT_INVALID_VALUE; k->max_blocks = value; break;
         case RT_TUNE_PERFRAME_SKY: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_sky = value; break;
         case RT_TUNE_WF_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->wf_refill_min = (uint32_t)value; break;

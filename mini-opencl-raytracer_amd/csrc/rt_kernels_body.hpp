@@ -1179,8 +1179,16 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 // from HBM/L2 (a.tileMajor) -- tile-major, a tile's frames back to back for
                 // coherent node and triangle fetches (profiles/r01/work_order_ab.txt)
                 uint32_t tile = unit >> 6;  // wave-uniform (scalar division)
-                uint32_t slot = 0;
-                if (fused && a.tileMajor) {
+                uint32_t slot = 0, pblk = 0, lf = 0;
+                // pixel-major (a.tileMajor 2; F = 2, 4 or 8 fused frames): a unit is 64 / F pixels of
+                // a tile x the F frames -- work item w at frame w % F of the unit's pixel w / F -- so
+                // a pixel's frames walk side by side in one wave
+                const bool pxMajor = fused && a.tileMajor == 2u;
+                if (pxMajor) {
+                    lf = (uint32_t)__builtin_ctz(a.nFrames);
+                    pblk = tile & (a.nFrames - 1u);
+                    tile >>= lf;
+                } else if (fused && a.tileMajor) {
                     slot = tile % a.nFrames;
                     tile /= a.nFrames;
                 } else if (fused) {
@@ -1190,8 +1198,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 if (state == kIdle && rank < take) {
                     const uint32_t w = used + rank;  // chunks are whole 8x8 tiles
                     const uint32_t ty = tile / a.tilesX, tx = tile - ty * a.tilesX;
-                    const uint32_t x = tx * 8u + (w & 7u),
-                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (w >> 3);
+                    uint32_t pix = w;  // pixel in the tile
+                    if (pxMajor) {
+                        slot = w & (a.nFrames - 1u);
+                        pix = (pblk << (6u - lf)) + (w >> lf);
+                    }
+                    const uint32_t x = tx * 8u + (pix & 7u),
+                                   row = a.rowBegin + (ty * a.bandPeriod + a.bandPhase) * 8u + (pix >> 3);
                     const uint64_t g64 = (uint64_t)row * a.width + x;
                     if (x < a.width && row < rowEnd && g64 >= a.gidBegin && g64 < a.gidEnd) {
                         gid = (uint32_t)g64;
