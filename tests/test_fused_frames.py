@@ -154,16 +154,17 @@ def test_overlapped_accumulation_stays_in_order(cornell):
     assert ga.tobytes() == gb.tobytes(), f"{(ga != gb).any(axis=1).sum()} pixels differ"
 
 
-@pytest.mark.parametrize("scene,n", [("cornell", 8), ("bunny", 8), ("cornell", 4), ("cornell", 2), ("cornell", 6)])
+@pytest.mark.parametrize("scene,n", [("cornell", 8), ("bunny", 8), ("cornell", 4), ("cornell", 2), ("cornell", 6),
+                                     ("cornell_lds", 8)])  # (cornell_lds: the LDS walk ignores the order)
 def test_fused_pixel_major_order(cornell, scene, n):
     """Pixel-major work order (tile_major 2, the default for large launches on scenes in HBM/L2): with F =
     2, 4 or 8 fused frames a work unit is 64 / F pixels of a tile x the F frames, a pixel's frames side by
     side in a wave; other F fall back to tile-major -- same bits as per-frame launches, with band
     interleaves."""
     from clrt import proxy
-    sc = cornell if scene == "cornell" else proxy.bunny_proxy()
+    sc = proxy.bunny_proxy() if scene == "bunny" else cornell
     W, H = 248, 136
-    kw = dict(force_global=True, interleave=(2, 1)) if scene == "cornell" else {}
+    kw = {"cornell": dict(force_global=True, interleave=(2, 1)), "bunny": {}, "cornell_lds": dict(interleave=(2, 1))}[scene]
     _same(_render(sc, W, H, 2, n, True, tuning={"tile_major": 2}, **kw), _render(sc, W, H, 2, n, False, **kw))
 
 
