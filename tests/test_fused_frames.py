@@ -155,7 +155,7 @@ def test_overlapped_accumulation_stays_in_order(cornell):
 
 
 @pytest.mark.parametrize("scene,n", [("cornell", 8), ("bunny", 8), ("cornell", 4), ("cornell", 2), ("cornell", 6),
-                                     ("cornell_lds", 8)])  # (cornell_lds: the LDS walk ignores the order)
+                                     ("cornell_lds", 8), ("cornell_g64", 4)])  # (cornell_lds: the LDS walk ignores the order)
 def test_fused_pixel_major_order(cornell, scene, n):
     """Pixel-major work order (tile_major 2, the default for large launches on scenes in HBM/L2): with F =
     2, 4 or 8 fused frames a work unit is 64 / F pixels of a tile x the F frames, a pixel's frames side by
@@ -164,8 +164,10 @@ def test_fused_pixel_major_order(cornell, scene, n):
     from clrt import proxy
     sc = proxy.bunny_proxy() if scene == "bunny" else cornell
     W, H = 248, 136
-    kw = {"cornell": dict(force_global=True, interleave=(2, 1)), "bunny": {}, "cornell_lds": dict(interleave=(2, 1))}[scene]
-    _same(_render(sc, W, H, 2, n, True, tuning={"tile_major": 2}, **kw), _render(sc, W, H, 2, n, False, **kw))
+    kw = {"cornell": dict(force_global=True, interleave=(2, 1)), "bunny": {}, "cornell_lds": dict(interleave=(2, 1)),
+          "cornell_g64": dict(force_global=True)}[scene]
+    tune = {"tile_major": 2, **({"global_oct": 0} if scene == "cornell_g64" else {})}  # (g64: the 64-B global records)
+    _same(_render(sc, W, H, 2, n, True, tuning=tune, **kw), _render(sc, W, H, 2, n, False, **kw))
 
 
 @pytest.mark.parametrize("force_global", [False, True])
