@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase wave-cycle shares of the step schedule (stats variant, s_memtime).
-Usage: phase_profile.py [step]"""
+Usage: phase_profile.py [step]   (env: RT_PHASE_SCENE=bunny, RT_PHASE_MATH, RT_PHASE_LB, RT_PHASE_FRAMES,
+RT_PHASE_TUNE=name=value,...)"""
 import os
 import sys
 
@@ -25,6 +26,8 @@ for name in scheds:
   for math in maths:
     for lb in lbs:
         r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=sched)
+        for t in filter(None, os.environ.get("RT_PHASE_TUNE", "").split(",")):  # name=value,...
+            r.k.set_tuning(t.split("=")[0], int(t.split("=")[1]))
         nf = int(os.environ.get("RT_PHASE_FRAMES", "8"))
         r.frame(1, light_bounces=lb, n_frames=nf if nf > 1 else None)
         r.ctx.Finish()
