@@ -78,7 +78,8 @@ TUNING = {"refill_min": 0, "shade_min": 1, "refill_min_global": 2, "shade_min_gl
           "bulk_percent": 8, "top_nodes": 9,
           "tile_major": 13, "perframe_sky": 14, "wf_refill_min": 15, "wf_streams_per_cu": 16,
           "wf_top_nodes": 17, "global_oct": 18, "perframe_defer": 19, "max_blocks": 20,
-          "perframe_defer_min": 21, "perframe_batch": 23}
+          "perframe_defer_min": 21, "perframe_batch": 23, "step_weight_node_global": 24,
+          "step_weight_leaf_global": 25}
 
 
 class Stats(ctypes.Structure):

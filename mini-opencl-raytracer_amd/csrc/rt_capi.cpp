@@ -63,6 +63,7 @@ struct rt_kernel_s {
     // profiles/r02/goct_sweep.txt)
     uint32_t refill_min_g = 0, shade_min_g = 0;
     uint32_t w_node = 35, w_leaf = 55;         // step schedule: node / triangle step cost weights
+    uint32_t w_node_g = 0, w_leaf_g = 0;       // ... on scenes read from HBM/L2 (0: auto)
     // pixels per work-counter fetch: bulk, and the cap of the launch-sized tail chunk (swept on
     // MI355X: profiles/r02/chunk_sweep.txt; 128 / 64 of round 1 left the counter at its atomic
     // throughput once sky tiles were decided at ring fill: 4K Cornell 1.01 -> 0.79 ms/frame)
@@ -1092,6 +1093,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     }
     a.refillMin = lds ? k->refill_min : k->refill_min_g ? k->refill_min_g : goct ? 16u : 8u;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g ? k->shade_min_g : 48u;
+    if (!lds) {
+        // scenes in HBM/L2: a node step's loads cost more against a triangle step's than in LDS
+        // (octant walk under the pixel-major order: 45 / 55, profiles/r05/goct_bursts_weights.txt)
+        a.stepWeightNode = k->w_node_g ? k->w_node_g : goct ? 45u : k->w_node;
+        a.stepWeightLeaf = k->w_leaf_g ? k->w_leaf_g : k->w_leaf;
+    }
     if (wf) a.nTop = std::min(a.nTop, k->wf_top_limit);
     const size_t smem =
         wf ? (lds ? ((size_t)a.octRecords + 3 * (size_t)k->n_tris) * 16 : (size_t)a.nTop * 64) +
@@ -1655,6 +1662,8 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_PERFRAME_DEFER: if (!in(0, 2)) return RT_INVALID_VALUE; k->pf_defer = value; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: if (value < 0) return RT_INVALID_VALUE; k->pf_defer_min = (uint32_t)value; break;
         case RT_TUNE_PERFRAME_BATCH: if (!in(1, (int)rtk::kMaxFusedFrames)) return RT_INVALID_VALUE; k->pf_batch = (uint32_t)value; break;
+        case RT_TUNE_STEP_WEIGHT_NODE_GLOBAL: if (!in(0, 1000)) return RT_INVALID_VALUE; k->w_node_g = (uint32_t)value; break;
+        case RT_TUNE_STEP_WEIGHT_LEAF_GLOBAL: if (!in(0, 1000)) return RT_INVALID_VALUE; k->w_leaf_g = (uint32_t)value; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
@@ -1684,6 +1693,8 @@ int rtKernelGetTuning(rt_kernel k, int param, int* value) {
         case RT_TUNE_PERFRAME_DEFER: *value = k->pf_defer; break;
         case RT_TUNE_PERFRAME_DEFER_MIN: *value = (int)k->pf_defer_min; break;
         case RT_TUNE_PERFRAME_BATCH: *value = (int)k->pf_batch; break;
+        case RT_TUNE_STEP_WEIGHT_NODE_GLOBAL: *value = (int)k->w_node_g; break;
+        case RT_TUNE_STEP_WEIGHT_LEAF_GLOBAL: *value = (int)k->w_leaf_g; break;
         default: return RT_INVALID_VALUE;
     }
     return RT_SUCCESS;
