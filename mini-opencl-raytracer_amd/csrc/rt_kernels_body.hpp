@@ -765,10 +765,10 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_GTRI_BURST
 #define RT_GTRI_BURST RT_TRI_BURST
 #endif
-// ... and for the octant walk over HBM/L2 (node bursts of 3-5 tie, 6 is 1.7 % slower, 2 and 8
-// 1-2 %: profiles/r02/goct/burst_ab_bunny.txt)
+// ... and for the octant walk over HBM/L2: 5 under the pixel-major order (4: +1.1 %, 6: +0.6 %, 8: +1.0 %,
+// 3: +4.6 %; profiles/r05/goct_bursts_weights.txt; round 2's tile-major walk tied 3-5)
 #ifndef RT_ONODE_BURST
-#define RT_ONODE_BURST 4
+#define RT_ONODE_BURST 5
 #endif
 #ifndef RT_OTRI_BURST
 #define RT_OTRI_BURST RT_TRI_BURST
