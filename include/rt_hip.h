@@ -258,7 +258,7 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     auto: 16 / 48 walking octant records, 8 / 48 the 64-B records)
  *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)
  *   STEP_WEIGHT_NODE_GLOBAL / STEP_WEIGHT_LEAF_GLOBAL  the same for scenes read from HBM/L2 (0 =
- *                                     auto: 45 / 55 walking octant records, else the LDS weights)
+ *                                     auto: 65 / 55 walking octant records, else the LDS weights)
  *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64: bulk chunk
  *                                     (512) / largest tail chunk (256; a launch uses the largest
  *                                     power-of-two multiple of 64 up to it that gives every

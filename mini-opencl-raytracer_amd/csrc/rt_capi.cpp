@@ -1095,8 +1095,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     a.shadeMin = lds ? k->shade_min : k->shade_min_g ? k->shade_min_g : 48u;
     if (!lds) {
         // scenes in HBM/L2: a node step's loads cost more against a triangle step's than in LDS
-        // (octant walk under the pixel-major order: 45 / 55, profiles/r05/goct_bursts_weights.txt)
-        a.stepWeightNode = k->w_node_g ? k->w_node_g : goct ? 45u : k->w_node;
+        // (octant walk under the pixel-major order: 65 / 55 -- 35: +1.0 %, 45: +0.4 %, 80-130 the same;
+        // profiles/r05/goct_bursts_weights.txt)
+        a.stepWeightNode = k->w_node_g ? k->w_node_g : goct ? 65u : k->w_node;
         a.stepWeightLeaf = k->w_leaf_g ? k->w_leaf_g : k->w_leaf;
     }
     if (wf) a.nTop = std::min(a.nTop, k->wf_top_limit);
