@@ -255,7 +255,7 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *                                     lanes are free (1-64, default 6); shade when this many are
  *                                     ready (1-64, default 48)
  *   REFILL_MIN_GLOBAL / SHADE_MIN_GLOBAL  the same for scenes read from HBM/L2 (0-64; default 0 =
- *                                     auto: 16 / 48 walking octant records, 8 / 48 the 64-B records)
+ *                                     auto: 32 / 48 walking octant records, 8 / 48 the 64-B records)
  *   STEP_WEIGHT_NODE / STEP_WEIGHT_LEAF   relative cost of a node / triangle step (35 / 55)
  *   STEP_WEIGHT_NODE_GLOBAL / STEP_WEIGHT_LEAF_GLOBAL  the same for scenes read from HBM/L2 (0 =
  *                                     auto: 65 / 55 walking octant records, else the LDS weights)

@@ -1091,7 +1091,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.octRecords = 2u * a.octB;
         a.nNodes = goct_word(k->n_nodes, RT_GOCT_GROUP);  // the END word
     }
-    a.refillMin = lds ? k->refill_min : k->refill_min_g ? k->refill_min_g : goct ? 16u : 8u;
+    // (octant walk: refill at 32 free lanes under the pixel-major order, 16 before: -0.5 %,
+    // profiles/r05/goct_bursts_weights.txt)
+    a.refillMin = lds ? k->refill_min : k->refill_min_g ? k->refill_min_g : goct ? 32u : 8u;
     a.shadeMin = lds ? k->shade_min : k->shade_min_g ? k->shade_min_g : 48u;
     if (!lds) {
         // scenes in HBM/L2: a node step's loads cost more against a triangle step's than in LDS
