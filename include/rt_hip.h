@@ -260,7 +260,8 @@ int rtValidateBVH(const void* nodes, size_t n_nodes, size_t n_tris, int* depth);
  *   STEP_WEIGHT_NODE_GLOBAL / STEP_WEIGHT_LEAF_GLOBAL  the same for scenes read from HBM/L2 (0 =
  *                                     auto: 65 / 55 walking octant records, else the LDS weights)
  *   CHUNK_PIXELS / TAIL_CHUNK         pixels per work-counter fetch, multiples of 64: bulk chunk
- *                                     (512) / largest tail chunk (256; a launch uses the largest
+ *                                     (0 = auto: 512, 1024 in the pixel-major order) / largest tail
+ *                                     chunk (256; a launch uses the largest
  *                                     power-of-two multiple of 64 up to it that gives every
  *                                     wave >= 2.5 tail chunks)
  *   BULK_PERCENT                      share of the work handed out in bulk chunks (80)

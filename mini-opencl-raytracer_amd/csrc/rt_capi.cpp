@@ -67,7 +67,7 @@ struct rt_kernel_s {
     // pixels per work-counter fetch: bulk, and the cap of the launch-sized tail chunk (swept on
     // MI355X: profiles/r02/chunk_sweep.txt; 128 / 64 of round 1 left the counter at its atomic
     // throughput once sky tiles were decided at ring fill: 4K Cornell 1.01 -> 0.79 ms/frame)
-    uint32_t chunk_pixels = 512, tail_chunk = 256;
+    uint32_t chunk_pixels = 0, tail_chunk = 256;  // chunk_pixels 0: auto (512; 1024 pixel-major)
     uint32_t bulk_percent = 80;                // share of the frame handed out in bulk chunks
     uint32_t band_period = 1, band_phase = 0;  // 8-row band interleave (multi-GPU sharding)
     uint32_t* work_counter = nullptr;  // persistent schedules' chunk counters: [4] per render stream
@@ -1006,7 +1006,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     if (n_tiles * 64 > 0xfff00000ull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
     a.workCounter = k->work_counter + 4 * RT_RAD_SETS;  // per-frame launches: their own counters
-    a.chunkPixels = k->chunk_pixels;
+    a.chunkPixels = k->chunk_pixels ? k->chunk_pixels : 512u;  // (the launch's order decides below)
     a.tailChunk = k->tail_chunk;
     a.refillMin = k->refill_min;
     a.shadeMin = k->shade_min;
@@ -1156,10 +1156,14 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // (multi-GPU ranks: N = 8 renders 1/8 of the frame) get a larger tail (bulk 80 % -> ~37 %:
         // emulated N = 8 rank step, Cornell 1.112 -> 1.047 ms, bunny proxy 1.694 -> 1.629 ms;
         // profiles/r02/multigpu/n8_chunk_sweep_*.txt); full 4K launches keep 80 %
+        // bulk chunks of 512 work items, 1024 in the pixel-major order (two whole tiles x 8 frames per
+        // fetch: bunny proxy -0.8 %, profiles/r05/goct_bursts_weights.txt)
+        const uint32_t chunk = k->chunk_pixels ? k->chunk_pixels : a.tileMajor == 2u ? 1024u : 512u;
+        a.chunkPixels = chunk;
         uint64_t bulk = tot * k->bulk_percent / 100;
-        const uint64_t reserve = 2u * waves * k->chunk_pixels;
+        const uint64_t reserve = 2u * waves * chunk;
         bulk = std::min<uint64_t>(bulk, tot > reserve ? tot - reserve : 0u);
-        a.chunkSplit = tot >= 2u * waves * k->chunk_pixels ? (uint32_t)(bulk / k->chunk_pixels * k->chunk_pixels) : 0u;
+        a.chunkSplit = tot >= 2u * waves * chunk ? (uint32_t)(bulk / chunk * chunk) : 0u;
         // tail chunks: the largest power-of-two multiple of 64 pixels, up to tail_chunk, that still
         // gives every wave >= 2.5 of them -- few atomics on the tail counter for large launches,
         // fine-grained balance for small ones (4K fused 256, 4K per-frame / 1080p / 512^2 fused 128,
@@ -1646,7 +1650,7 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
         case RT_TUNE_STEP_WEIGHT_NODE: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_node = (uint32_t)value; break;
         case RT_TUNE_STEP_WEIGHT_LEAF: if (!in(1, 1000)) return RT_INVALID_VALUE; k->w_leaf = (uint32_t)value; break;
         case RT_TUNE_CHUNK_PIXELS:
-            if (!in(64, 4096) || value % 64) return RT_INVALID_VALUE;
+            if (!in(0, 4096) || value % 64) return RT_INVALID_VALUE;  // (0: auto)
             k->chunk_pixels = (uint32_t)value;
             break;
         case RT_TUNE_TAIL_CHUNK:
