@@ -98,3 +98,26 @@ def test_retired_schedules_and_tunings_are_refused(cornell):
     r.frame(1, light_bounces=2)
     assert np.isfinite(r.result()).all()
     r.close()
+
+
+def test_round5_tuning_ranges(cornell):
+    """Round-5 tunings: TILE_MAJOR takes -1..2 (2: pixel-major), CHUNK_PIXELS takes 0 (auto) or multiples
+    of 64 up to 4096, the HBM/L2 step weights take 0 (auto) ..1000; out-of-range values are refused and
+    leave the setting as it was; 22 (the retired speculative walk) stays refused."""
+    r = HipRenderer(cornell, 64, 48)
+    lib, h = r.k._lib, r.k.handle
+    ok = [(N.TUNING["tile_major"], v) for v in (-1, 0, 1, 2)] + \
+         [(N.TUNING["chunk_pixels"], v) for v in (0, 64, 1024, 4096)] + \
+         [(N.TUNING["step_weight_node_global"], v) for v in (0, 1, 1000)] + \
+         [(N.TUNING["step_weight_leaf_global"], v) for v in (0, 65)]
+    for tid, v in ok:
+        assert lib.rtKernelSetTuning(h, tid, v) == 0, (tid, v)
+        assert r.k.get_tuning([k for k, i in N.TUNING.items() if i == tid][0]) == v
+    bad = [(N.TUNING["tile_major"], 3), (N.TUNING["tile_major"], -2), (N.TUNING["chunk_pixels"], 96),
+           (N.TUNING["chunk_pixels"], 8192), (N.TUNING["step_weight_node_global"], 1001),
+           (N.TUNING["step_weight_leaf_global"], -1), (22, 1)]
+    for tid, v in bad:
+        assert lib.rtKernelSetTuning(h, tid, v) == -30, (tid, v)
+    r.frame(1, light_bounces=2)
+    assert np.isfinite(r.result()).all()
+    r.close()
