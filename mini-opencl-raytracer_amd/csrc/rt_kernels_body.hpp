@@ -510,7 +510,7 @@ struct LaneStats {
 // The body of Render's bounce loop after Intersect (kernel_bvh.cl:358-380): radiance and
 // beta updates, BRDF sample and the next ray.  Returns false where the reference breaks
 // out of the loop (miss, or pdf <= 0 / NaN).
-template <class M, bool kStats>
+template <class M, bool kStats, bool kScalarRec = false>
 __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& radiance, F3& beta,
                                              uint32_t& seed, const SceneView& sc, const KernelArgs& a,
                                              LaneStats& st) {
@@ -524,15 +524,39 @@ __device__ __forceinline__ bool shade_bounce(const Traversal& h, Ray& ray, F3& r
     typedef float v4f __attribute__((ext_vector_type(4)));
     typedef float v2f __attribute__((ext_vector_type(2)));
     const float4* rec = sc.stris + 3 * h.prim;
-    const v4f s1 = *reinterpret_cast<const v4f*>(rec), s2 = *reinterpret_cast<const v4f*>(rec + 1);
-    const v2f s3 = *reinterpret_cast<const v2f*>(rec + 2);
+    v4f s1, s2;
+    v2f s3;
+    // (records in HBM/L2, kScalarRec: a round whose lanes all hit one triangle, or all use one
+    // material, reads that record through the scalar cache -- oct_step_g; bunny proxy -0.3 %,
+    // profiles/r05/goct_scalar_ab.txt)
+    const uint32_t p0 = kScalarRec ? (uint32_t)__builtin_amdgcn_readfirstlane(h.prim) : 0u;
+    if (kScalarRec && __ballot((uint32_t)h.prim != p0) == 0ull) {
+        const cv4f* cp = (const cv4f*)(sc.stris + 3u * p0);
+        s1 = cp[0];
+        s2 = cp[1];
+        s3 = *((__attribute__((address_space(4))) const v2f*)(sc.stris + 3u * p0 + 2u));
+    } else {
+        s1 = *reinterpret_cast<const v4f*>(rec);
+        s2 = *reinterpret_cast<const v4f*>(rec + 1);
+        s3 = *reinterpret_cast<const v2f*>(rec + 2);
+    }
     const float w = (1.0f - h.u) - h.v;
     const F3 normal = normalize<M>(
         madd<M>(F3{s1.x, s1.y, s1.z}, w, madd<M>(F3{s2.x, s2.y, s2.z}, h.u, F3{s2.w, s3.x, s3.y} * h.v)));
     const F3 pos = madd<M>(ray.d, h.t, ray.o);
     const uint32_t mi = 4u * __float_as_uint(s1.w);
-    const v4f m0 = *reinterpret_cast<const v4f*>(sc.smats + mi), m1 = *reinterpret_cast<const v4f*>(sc.smats + mi + 1),
-              m2 = *reinterpret_cast<const v4f*>(sc.smats + mi + 2);
+    v4f m0, m1, m2;
+    const uint32_t mi0 = kScalarRec ? __builtin_amdgcn_readfirstlane(mi) : 0u;
+    if (kScalarRec && __ballot(mi != mi0) == 0ull) {
+        const cv4f* cp = (const cv4f*)(sc.smats + mi0);
+        m0 = cp[0];
+        m1 = cp[1];
+        m2 = cp[2];
+    } else {
+        m0 = *reinterpret_cast<const v4f*>(sc.smats + mi);
+        m1 = *reinterpret_cast<const v4f*>(sc.smats + mi + 1);
+        m2 = *reinterpret_cast<const v4f*>(sc.smats + mi + 2);
+    }
     MatView m{F3{m0.x, m0.y, m0.z}, F3{m1.x, m1.y, m1.z}, F3{m2.x, m2.y, m2.z}, m0.w, m1.w, m2.w};
 
     radiance = madd<M>(beta * m.emission, 50.0f, radiance);
@@ -1411,7 +1435,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     a.hitT[gid - (fused ? last : 0u)] = h.t;
                 }
             }
-            const bool more = shade_bounce<M, kStats>(h, ray, radiance, beta, seed, sc, a, st);
+            const bool more = shade_bounce<M, kStats, kGlobalOct>(h, ray, radiance, beta, seed, sc, a, st);
             ++bounce;
             if (!more || bounce >= bounces) {
                 radiance = F3{M::max(radiance.x, 0.0f), M::max(radiance.y, 0.0f), M::max(radiance.z, 0.0f)};
