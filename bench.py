@@ -60,7 +60,7 @@ CAMERA = ((0.0, -25.0, 8.5), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
 PMC_PATH = os.path.join(REPO, "profiles", "pmc.json")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -93,6 +93,8 @@ def parse():
     p.add_argument("--no-drop-in", action="store_true",
                    help="skip the extra per-frame (drop-in RenderFrame loop) measurement reported beside "
                         "the fused headline at N = 1")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the other BASELINE configs timed after the headline at N = 1 (the `configs` key)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--gather-sync", action="store_true",
                    help="N>1: wait for each step's gather before queueing the next step (no pipelining)")
@@ -112,7 +114,7 @@ def parse():
     p.add_argument("--fail-links", action="store_true",
                    help="test hook (rtCommSetOption RT_COMM_OPT_FAIL_LINKS): this rank reports its copy-engine "
                         "links as broken, so the world takes the RCCL fallback -- which the line then reports")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 class Rank:
@@ -152,6 +154,13 @@ class Rank:
     def finish(self):
         self.ctx.Finish()
 
+    def release(self):
+        self.finish()
+        self.k.release()
+        for b in self.bufs + [self.out]:
+            b.release()
+        self.ctx.release()
+
 
 def make_kernel(ctx, bufs, out, args):
     k = clrt.CLKernel(ctx, "KernelEntry")
@@ -174,6 +183,83 @@ def make_kernel(ctx, bufs, out, args):
         name, value = t.split("=", 1)
         k.set_tuning(name, int(value))
     return k
+
+
+def load_scene(args, device=0):
+    if args.scene == "bunny":
+        from clrt import proxy as clrt_proxy
+        scene = clrt_proxy.bunny_proxy()
+    else:
+        scene = clrt.scene.cornell()
+    if args.bvh.startswith("device"):  # SURVEY 8(f.4): BVH built on the GPU (rtBuildBVHEx)
+        if args.scene == "bunny":
+            raw = clrt.scene.load_obj(os.path.join(clrt_proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
+            ft, fm = raw.triangles, raw.materials
+        else:
+            z = np.load(clrt.scene.CORNELL_NPZ, allow_pickle=False)
+            ft, fm = z["triangles"].view(N.TRIANGLE_DTYPE), z["materials"].view(N.MATERIAL_DTYPE)
+        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=device,
+                                            method="lbvh" if args.bvh == "device-lbvh" else "ploc")
+    return scene
+
+
+# The other BASELINE configs, timed in the same N = 1 run after the headline (rank 0 only): each
+# on its own context with its own count pass, warm-up and timed loop, priced by its own PMC key.
+# `value` stays the headline's (config 3).  Config 1 is the reference's CPU-only plumbing case
+# and config 4 the 8-GPU run (the driver's scaling bench).
+EXTRA_CONFIGS = (
+    ("cfg5_bunny", {"scene": "bunny"}, 10,
+     "BASELINE config 5 on one GPU: the bunny-class proxy (69,692 triangles, 48k-node BVH in HBM/L2), "
+     "3840x2160, 8 spp, 9 bounces"),
+    ("cfg2_1080p", {"width": 1920, "height": 1080, "bounces": 2, "frames": 1}, 40,
+     "BASELINE config 2: 1920x1080 Cornell, 1 spp, 2 bounces (primary + one secondary ray per pixel: "
+     "the reference has no shadow rays, SURVEY.md 7 hard part 6)"),
+    ("cfg3_pinned", {"math": "pinned"}, 10,
+     "BASELINE config 3 in the CPU-parity math (pinned: bit-exact with the reference kernel built for the "
+     "CPU, tests/test_ref_cpu.py, tests/test_gpu_parity.py)"),
+)
+
+
+def time_config(over, steps, device):
+    """One extra config: its own context, count pass, 2 warm-up steps and `steps` timed steps."""
+    a = parse([])
+    a.__dict__.update(over)
+    r = Rank(load_scene(a, device), a, device)
+    st = count_pass(r)
+    local_counts = np.array([st["rays"], st["node_visits"], st["tri_tests"], st["hits"]], np.float64)
+    for _ in range(2):
+        r.render()
+    r.k.set_timing(True)
+    r.k.reset_stats()
+    r.finish()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.render()
+    r.finish()
+    dt = time.perf_counter() - t0
+    ks = r.k.stats()
+    r.k.set_timing(False)
+    launches = max(1, ks["launches"])
+    fpl = a.frames if a.launch == "fused" else 1
+    period = ks["render_period_ms"] if fpl > 1 else 0.0
+    rl = roofline(a, 1, fpl, ks["kernel_ms"] / launches, period, local_counts, r.pixels)
+    r.release()
+    ms_step = dt * 1e3 / steps
+    return {"workload": f"{a.scene} {a.width}x{a.height} {a.frames}spp {a.bounces}-bounce path trace",
+            "math": a.math, "steps": steps, "ms_per_step": round(ms_step, 4),
+            "ms_per_frame": round(ms_step / a.frames, 4),
+            "value": round(local_counts[0] * steps / dt / 1e6, 3), "unit": "Mrays/s",
+            "rays_per_step": int(local_counts[0]), "roofline": rl}
+
+
+def extra_configs(device):
+    out = {}
+    for name, over, steps, desc in EXTRA_CONFIGS:
+        t0 = time.perf_counter()
+        out[name] = {"config": desc, **time_config(over, steps, device),
+                     "wall_s": None}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+    return out
 
 
 def count_pass(r):
@@ -311,6 +397,18 @@ def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts,
         # CUs against the busy cycles summed over the 8 XCDs -- the HBM/L2 octant walk's binding
         # resource (VALU issue is not: DESIGN.md section 5)
         rl["ta_busy"] = round(e["TA_TA_BUSY_sum"] / 256.0 / (e["GRBM_GUI_ACTIVE"] / 8.0), 4)
+    acc = e.get("accum")
+    if acc and "SQ_INSTS_VALU" in acc:
+        # the fused launch's accumulation (accum_frames, one per render launch) issues on the same
+        # SIMDs while the next render runs: its VALU, and both kernels' VALU over the render period
+        ai = acc["SQ_INSTS_VALU"]
+        rl["accum_valu_insts_per_launch"] = int(ai)
+        rl["accum_lane_util"] = (round(acc["SQ_THREAD_CYCLES_VALU"] / (64.0 * ai), 4)
+                                 if "SQ_THREAD_CYCLES_VALU" in acc and ai else None)
+        rl["frac_with_accum"] = round((insts + ai) / (kernel_ms * 1e-3) / VALU_PEAK, 4)
+    else:
+        rl["accum_valu_insts_per_launch"] = None
+        rl["frac_with_accum"] = None
     rl["pmc"] = {"file": "profiles/pmc.json", "key": key, "valu_insts_per_launch": int(insts),
                  "kernel_ms_in_pmc_pass": e.get("kernel_ms"), "source_hash": e.get("source_hash"),
                  "stale": e.get("source_hash") != src}
@@ -351,20 +449,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
-    if args.scene == "bunny":
-        from clrt import proxy as clrt_proxy
-        scene = clrt_proxy.bunny_proxy()
-    else:
-        scene = clrt.scene.cornell()
-    if args.bvh.startswith("device"):  # SURVEY 8(f.4): BVH built on the GPU (rtBuildBVHEx)
-        if args.scene == "bunny":
-            raw = clrt.scene.load_obj(os.path.join(clrt_proxy.GEN_DIR, "bunny_proxy.obj"), build=False)
-            ft, fm = raw.triangles, raw.materials
-        else:
-            z = np.load(clrt.scene.CORNELL_NPZ, allow_pickle=False)
-            ft, fm = z["triangles"].view(N.TRIANGLE_DTYPE), z["materials"].view(N.MATERIAL_DTYPE)
-        scene = clrt.scene.build_bvh_device(ft, fm, 4, device=local,
-                                            method="lbvh" if args.bvh == "device-lbvh" else "ploc")
+    scene = load_scene(args, local)
 
     comm = None
     shared_dir = None
@@ -511,6 +596,8 @@ def main():
         line["check_gather"] = check
     if world == 1 and comm is None and args.launch == "fused" and not args.no_drop_in:
         line["drop_in"] = drop_in(r, args, rays_per_step, steps=args.steps)
+    if world == 1 and comm is None and not args.no_configs:
+        line["configs"] = extra_configs(local)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(scene, args, pinned_rays(r, args))
     print(json.dumps(line))

@@ -463,6 +463,14 @@ int rtCommGetStatus(rt_comm comm, rt_comm_status* out);
  * broken at the next plan's link step, so the world takes the RCCL fallback (what a world whose
  * IPC mappings or trial round fail does). */
 #define RT_COMM_OPT_FAIL_LINKS 1
+/* RT_COMM_OPT_REPLAN_PERIOD (value 2): gathers per plan before the world re-plans collectively
+ * (default 65,534, the flag values a copy-engine plan holds; 1 .. 65,534; every rank of the world
+ * must set the same value before its next gather).  RT_COMM_OPT_SYSTEM_ACQUIRE (value 3): the
+ * root's first read of a gathered image runs its system-scope acquire (L1 + every XCD's L2) even
+ * when every writer is on the root's device -- it always does when another device's copy engines
+ * write the image. */
+#define RT_COMM_OPT_REPLAN_PERIOD 2
+#define RT_COMM_OPT_SYSTEM_ACQUIRE 3
 int rtCommSetOption(rt_comm comm, int option, int value);
 /* Blocking reductions of `count` doubles per local rank (values: n_local x count, in place),
  * op RT_COMM_SUM or RT_COMM_MAX; rtCommBarrier = a one-value reduction. */

@@ -107,6 +107,8 @@ COMM_TRANSPORT_NAMES = {-1: "none", COMM_TRANSPORT_COPY_ENGINES: "copy engines",
 COMM_FALLBACK_NAMES = {0: None, 1: "no peer access", 2: "IPC handle export/map failed",
                        3: "link trial round failed"}
 COMM_OPT_FAIL_LINKS = 1  # test hook (rtCommSetOption)
+COMM_OPT_REPLAN_PERIOD = 2  # gathers per plan before a collective re-plan (rtCommSetOption)
+COMM_OPT_SYSTEM_ACQUIRE = 3  # force the root's system-scope acquire after a gather (rtCommSetOption)
 
 
 class CommStatus(ctypes.Structure):

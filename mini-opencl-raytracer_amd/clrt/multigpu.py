@@ -202,7 +202,7 @@ class Comm:
                 "gathers": st.gathers, "last_xfer_ms": None if st.last_xfer_ms < 0 else st.last_xfer_ms}
 
     def set_option(self, option: int, value: int) -> None:
-        """rtCommSetOption (test hooks: N.COMM_OPT_FAIL_LINKS)."""
+        """rtCommSetOption (N.COMM_OPT_FAIL_LINKS, N.COMM_OPT_REPLAN_PERIOD, N.COMM_OPT_SYSTEM_ACQUIRE)."""
         check(self._lib.rtCommSetOption(self.handle, option, value), "comm option")
 
     def shard(self, kernel) -> None:

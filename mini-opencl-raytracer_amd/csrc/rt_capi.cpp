@@ -1141,7 +1141,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // (profiles/r05/pixel_major_ab.txt); else tile-major for large launches (a tile's frames back
         // to back: -1.4 %, profiles/r01/work_order_ab.txt) and frame-major for small ones (tile-major
         // bunches a costly tile's frames into the tail); LDS scenes frame-major (the ray ring)
-        const bool pow2 = n_frames == 2 || n_frames == 4 || n_frames == 8;
+        // (the pixel-major order is the step schedule's: the wavefront extend launches keep the
+        // big / frame-major rule their order was measured with, profiles/r02/wavefront/)
+        const bool pow2 = (n_frames == 2 || n_frames == 4 || n_frames == 8) && si == RT_SCHED_STEP;
         const bool big = !lds && tot >= 4096u * waves;
         a.tileMajor = n_frames < 2 ? 0u
                       : k->tile_major == 2 ? (!lds && pow2 ? 2u : 1u)

@@ -69,7 +69,9 @@ namespace {
 constexpr unsigned kBandRows = 8;     // = the 8x8 tile height of the persistent schedules
 constexpr size_t kPixelBytes = 16;    // one float3 slot of the output buffer
 constexpr size_t kProbeBytes = 4096;  // per rank, the trial round's copy
-constexpr uint64_t kFlagValues = 1ull << 22;  // flag values 0 .. kFlagValues - 1 (32 MB per rank)
+// flag values 0 .. kFlagValues - 1 (512 KB per rank): the world re-plans, collectively, every
+// kFlagValues - 2 gathers (ensure_plan), a few milliseconds once per 65k steps
+constexpr uint64_t kFlagValues = 1ull << 16;
 
 int map_nccl(ncclResult_t r) {
     switch (r) {
@@ -144,6 +146,12 @@ struct rt_comm_s {
     bool ipc_linked = false;         // ... with its links exchanged as IPC handles (link_ipc)
     int fallback_reason = RT_COMM_FALLBACK_NONE;  // the plan wanted the copy engines and runs RCCL
     bool fail_links = false;         // test hook (RT_COMM_OPT_FAIL_LINKS)
+    uint64_t replan_after = kFlagValues - 2;  // gathers per plan (RT_COMM_OPT_REPLAN_PERIOD)
+    // root: other devices' copy engines write its destination, so its first read of a gathered
+    // image runs a system-scope acquire on every XCD first (join_gather; RT_COMM_OPT_SYSTEM_ACQUIRE
+    // forces it on one device)
+    bool remote_writers = false;
+    bool force_acquire = false;
     uint64_t seq = 0;                // gathers enqueued with this plan (1, 2, ...)
     // ---- copy engines ----
     rt_mem target = nullptr;         // root: the plan's destination (pinned)
@@ -312,6 +320,15 @@ int flag_values(rt_comm c) {
     return map_hip(e);
 }
 
+// A system-scope acquire on the CU each workgroup runs on: its L1 and its XCD's L2 drop what they
+// cached of memory that another device may have written (buffer_inv sc0 sc1 on gfx950).  One
+// workgroup per CU: the dispatcher deals workgroups round-robin over the 8 XCDs, so every XCD's L2
+// sees at least one (the kernel itself reads and writes nothing).
+__global__ void system_acquire_kernel() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed when the wave ends
+}
+
 // a flag word (another device's, or this one's) := v, on the copy engine of stream s
 hipError_t flag_copy(rt_comm c, uint64_t* dst, uint64_t v, hipStream_t s) {
     return hipMemcpyAsync(dst, c->vals + v, sizeof(uint64_t), hipMemcpyDeviceToDeviceNoCU, s);
@@ -335,7 +352,7 @@ void free_buffers(rt_comm c) {
     if (c->target) rti::unpin(c->target);
     c->target = nullptr;
     c->runs.clear();
-    c->ce = c->ipc_linked = c->sends = false;
+    c->ce = c->ipc_linked = c->sends = c->remote_writers = false;
     c->fallback_reason = RT_COMM_FALLBACK_NONE;
     c->seq = c->join_seq = 0;
     c->xt_valid = false;
@@ -401,7 +418,7 @@ void quiesce(rt_comm c) {
 int ensure_plan(rt_comm c, unsigned W, unsigned H, int root, rt_mem dst, rt_mem out, bool* built) {
     *built = false;
     if (c->W == W && c->H == H && c->root == root && (c->rank != root || !c->ce || dst == c->target) &&
-        c->seq + 2 < kFlagValues)
+        c->seq < c->replan_after)
         return RT_SUCCESS;
     *built = true;
     quiesce(c);
@@ -471,6 +488,7 @@ int link_direct(const rt_comm* comms, int n_local, int root) {
     for (int i = 0; i < n_local; ++i) {
         comms[i]->peer_target = static_cast<uint8_t*>(R->target->dptr);
         comms[i]->ce = true;
+        if (comms[i]->ctx->device != R->ctx->device) R->remote_writers = true;
     }
     return RT_SUCCESS;
 }
@@ -686,6 +704,9 @@ int link_ipc(rt_comm c) {
         return rccl_buffers(c);
     }
     c->ce = c->ipc_linked = true;
+    // one process per GPU (an RCCL world): the other ranks' copy engines write the root's image
+    // from other devices (a shared world's ranks all run on one)
+    c->remote_writers = c->rank == c->root && c->nranks > 1 && c->fdir.empty();
     return RT_SUCCESS;
 }
 
@@ -932,6 +953,15 @@ int rtCommSetOption(rt_comm c, int option, int value) {
         c->fail_links = value != 0;
         return RT_SUCCESS;
     }
+    if (option == RT_COMM_OPT_REPLAN_PERIOD) {
+        if (value < 1 || (uint64_t)value > kFlagValues - 2) return RT_INVALID_VALUE;
+        c->replan_after = (uint64_t)value;
+        return RT_SUCCESS;
+    }
+    if (option == RT_COMM_OPT_SYSTEM_ACQUIRE) {
+        c->force_acquire = value != 0;
+        return RT_SUCCESS;
+    }
     return RT_INVALID_VALUE;
 }
 
@@ -994,6 +1024,13 @@ int rtCommEnqueueGatherBands(const rt_comm* comms, const rt_mem* outs, int n_loc
         }
         if (rc) return rc;
     }
+    // only a copy-engine plan writes into the destination it was built with: an RCCL plan (asked
+    // for, or a fallback) unpacks into whatever each call names, so it keeps no pin on the first one
+    for (int i = 0; fresh && i < n_local; ++i)
+        if (!comms[i]->ce && comms[i]->target) {
+            rti::unpin(comms[i]->target);
+            comms[i]->target = nullptr;
+        }
     bool ce = true;
     for (int i = 0; i < n_local; ++i) ce &= comms[i]->ce;
     // loopback and shared worlds move bytes on the copy engines only
@@ -1202,6 +1239,11 @@ int ce_gather(const rt_comm* comms, int n_local, int root, const rt_mem* outs) {
             for (int j = 0; j < n_local && e == hipSuccess; ++j)
                 if (comms[j] != R) e = hipStreamWaitEvent(R->ustream, comms[j]->sent[comms[j]->slot ^ 1], 0);
             if (e == hipSuccess && R->sends) e = hipStreamWaitEvent(R->ustream, R->dsent, 0);
+            if (e == hipSuccess && (R->remote_writers || R->force_acquire)) {  // (see join_gather)
+                hipLaunchKernelGGL(system_acquire_kernel, dim3(R->ctx->num_cus > 0 ? R->ctx->num_cus : 256), dim3(64), 0,
+                                   R->ustream);
+                e = hipGetLastError();
+            }
             if (e == hipSuccess) e = hipEventRecord(R->ctx->gtail, R->ustream);
             if (e != hipSuccess) return map_hip(e);
             R->ctx->gpending = true;
@@ -1261,13 +1303,21 @@ int finish_gather(const rt_comm* comms, int n_local, int root, rt_mem root_dst, 
 
 // The root's first read of a gathered image: `s` waits for every rank's arrival (flags between
 // processes, events within one; and the root's own copies), and the context's gather tail
-// becomes that point of `s`.
+// becomes that point of `s`.  Where other devices' copy engines wrote the image (remote_writers),
+// the root's caches may still hold lines of the previous image that the root read before (its
+// blits, kernels): a system-scope acquire on every XCD follows the waits, before any read.
+// (Multi-GPU byte parity of the direct-write gather has not been verified on hardware: every run
+// so far wrote from one device; RT_COMM_OPT_SYSTEM_ACQUIRE runs the acquire there, tests/test_comm.py.)
 hipError_t rti::join_gather(rt_comm c, hipStream_t s) {
     hipError_t e = hipSetDevice(c->ctx->device);
     for (int q = 0; c->ipc_linked && q < c->nranks && e == hipSuccess; ++q)
         if (q != c->root) e = hipStreamWaitValue64(s, c->rflags + q, c->join_seq, hipStreamWaitValueGte, ~0ull);
     for (size_t j = 0; j < c->join_events.size() && e == hipSuccess; ++j) e = hipStreamWaitEvent(s, c->join_events[j], 0);
     if (e == hipSuccess && c->sends) e = hipStreamWaitEvent(s, c->dsent, 0);
+    if (e == hipSuccess && (c->remote_writers || c->force_acquire)) {
+        hipLaunchKernelGGL(system_acquire_kernel, dim3(c->ctx->num_cus > 0 ? c->ctx->num_cus : 256), dim3(64), 0, s);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipEventRecord(c->ctx->gtail, s);
     return e;
 }

@@ -111,31 +111,36 @@ int flush_frames(rt_context ctx);
 // `s` waits for the root's pending gather arrivals (rt_comm.cpp; records gtail behind them)
 hipError_t join_gather(rt_comm c, hipStream_t s);
 
-// `s` waits for the gathers enqueued on the context so far (reads of a gathered image)
+// `s` waits for the gathers enqueued on the context so far (reads of a gathered image).  A join
+// that fails keeps its state (gjoin): the next read joins again, and the error is kept for the
+// next call that reports one (qs)
 inline hipError_t gather_wait(rt_context ctx, hipStream_t s) {
     hipError_t e = hipSuccess;
     if (ctx->gjoin) {
         e = join_gather(ctx->gjoin, s);  // (then gtail is the joining stream's tail)
+        if (e != hipSuccess) return e;
         ctx->gjoin = nullptr;
-        ctx->gpending = e == hipSuccess && s != ctx->stream;
+        ctx->gpending = s != ctx->stream;
         return e;
     }
     if (ctx->gpending) {
         e = hipStreamWaitEvent(s, ctx->gtail, 0);
-        if (s == ctx->stream) ctx->gpending = false;
+        if (e == hipSuccess && s == ctx->stream) ctx->gpending = false;
     }
     return e;
 }
 
 // The context's stream, after every pending accumulation and gather (see rt_context_s) and the
-// coalesced per-frame launches.
+// coalesced per-frame launches.  A failed wait is reported by the next call that returns a status
+// (ctx->pend_error).
 inline hipStream_t qs(rt_context ctx) {
     if (ctx->pend_k) (void)flush_frames(ctx);
     if (ctx->apending) {
         (void)hipStreamWaitEvent(ctx->stream, ctx->atail, 0);
         ctx->apending = false;
     }
-    (void)gather_wait(ctx, ctx->stream);
+    const hipError_t ge = gather_wait(ctx, ctx->stream);
+    if (ge != hipSuccess && ctx->pend_error == RT_SUCCESS) ctx->pend_error = map_hip(ge);
     ctx->mdirty = true;  // the caller enqueues on it
     return ctx->stream;
 }

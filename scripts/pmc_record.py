@@ -53,6 +53,13 @@ def main():
         for row in csv.DictReader(open(f)):
             if row["Name"] == k:
                 e["kernel_ms"] = float(row["AverageNs"]) / 1e6
+    # the fused launches' accumulation (accum_frames*, on its own stream beside the next render):
+    # its VALU shares the render's SIMDs, so the bench line prices it too (roofline.accum_*)
+    acc_k = [n for n in acc if "accum_frames" in n]
+    if acc_k:
+        a = {c: sum(v) / len(v) for c, v in acc[acc_k[0]].items()}
+        e["accum"] = {"kernel": acc_k[0], **{c: a[c] for c in ("SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU",
+                                                            "SQ_WAVE_CYCLES") if c in a}}
     e["source_hash"] = bench.kernel_source_hash()
     e["command"] = "python bench.py " + " ".join(bench_args)
     path = os.path.join(REPO, "profiles", "pmc.json")

@@ -9,7 +9,7 @@ NAME=$1; shift
 OUT=gpurun_out/pmc_$NAME
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in $*"
+B="python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in --no-configs $*"
 step() { local n=$1; shift; echo "== $n"; timeout -k 10 300 "$@" > $OUT/$n.log 2>&1; local rc=$?; echo "== $n rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/$n.log; exit $rc; }; }
 step trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B
 step fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p_fetch -o run -- $B
@@ -18,6 +18,6 @@ step sq1 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_INS
 step sq2 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d $OUT/p_sq2 -o run -- $B
 step wrq rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/p_wrq -o run -- $B
 step ta rocprofv3 --pmc TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum --output-format csv -d $OUT/p_ta -o run -- $B
-python scripts/pmc_record.py $OUT/trace $OUT/p_fetch $OUT/p_write $OUT/p_sq1 $OUT/p_sq2 $OUT/p_wrq $OUT/p_ta -- --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in "$@" > $OUT/record.txt
+python scripts/pmc_record.py $OUT/trace $OUT/p_fetch $OUT/p_write $OUT/p_sq1 $OUT/p_sq2 $OUT/p_wrq $OUT/p_ta -- --steps 1 --warmup 0 --no-cpu-baseline --no-drop-in --no-configs "$@" > $OUT/record.txt
 cp profiles/pmc.json $OUT/pmc.json
 tail -3 $OUT/record.txt

@@ -150,17 +150,25 @@ def test_gather_world_of_one(cornell, init, into_out, transport):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["copy", "copy-ipc"])
-def test_gather_images_read_by_kernels_are_current(cornell, transport):
+@pytest.mark.parametrize("transport,hooks", [("copy", ()), ("copy-ipc", ()), ("copy-ipc", ("acquire",)),
+                                             ("copy", ("acquire", "replan")), ("copy-ipc", ("replan",))])
+def test_gather_images_read_by_kernels_are_current(cornell, transport, hooks):
     """The copy engines write the root's image behind the GPU caches' back (SDMA, from another
     device's engine between GPUs): a kernel that reads the image after each gather -- here the
     runtime's 2-D blit copy, an L2-cached read of an image small enough to stay in L2 from one
-    step to the next -- must see that gather's bytes, never the previous step's lines."""
+    step to the next -- must see that gather's bytes, never the previous step's lines.  Hooks:
+    the root's system-scope acquire, which a root whose image other devices write runs before its
+    first read (RT_COMM_OPT_SYSTEM_ACQUIRE forces it here, on one device), and a collective
+    re-plan every second gather (RT_COMM_OPT_REPLAN_PERIOD: the flag values start over)."""
     import clrt
     W, H, steps = 256, 144, 6
     ctx = clrt.CLContext(0)
     comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
     comm.set_transport(N.COMM_TRANSPORT_COPY_ENGINES if transport == "copy" else N.COMM_TRANSPORT_COPY_ENGINES_IPC)
+    if "acquire" in hooks:
+        comm.set_option(N.COMM_OPT_SYSTEM_ACQUIRE, 1)
+    if "replan" in hooks:
+        comm.set_option(N.COMM_OPT_REPLAN_PERIOD, 2)
     bufs, out, k = _setup(ctx, cornell, W, H)
     comm.shard(k)
     dst = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
@@ -177,11 +185,58 @@ def test_gather_images_read_by_kernels_are_current(cornell, transport):
         k2.set_uint(N.FRAME_COUNT, 1 + 8 * step)
         ctx.ExecuteKernelFrames(k2, W * H, 8)
         assert got[step].tobytes() == _read(ctx, out2, W * H).tobytes(), f"step {step}: stale or torn image"
+    if "replan" in hooks:
+        assert comm.status()["gathers"] <= 2  # the plan was rebuilt every second gather
     comm.destroy()
     for b in bufs + bufs2 + [out, out2, dst] + snaps:
         b.release()
     k.release()
     k2.release()
+    ctx.release()
+
+
+@pytest.mark.gpu
+def test_comm_options_are_checked():
+    import clrt
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    for bad in (0, -1, 65535):
+        with pytest.raises(clrt.RTError):
+            comm.set_option(N.COMM_OPT_REPLAN_PERIOD, bad)
+    comm.set_option(N.COMM_OPT_REPLAN_PERIOD, 65534)
+    with pytest.raises(clrt.RTError):
+        comm.set_option(99, 1)
+    comm.destroy()
+    ctx.release()
+
+
+@pytest.mark.gpu
+def test_rccl_plan_does_not_hold_the_destination(cornell):
+    """An RCCL plan unpacks into whatever each gather names: a destination released after its
+    gather is not kept by the plan, and the next gather into another buffer needs no re-plan."""
+    import clrt
+    W, H = 320, 200
+    ctx = clrt.CLContext(0)
+    comm = mg.Comm.init_rank(ctx, 1, mg.Comm.unique_id(), 0)
+    comm.set_transport(N.COMM_TRANSPORT_RCCL)
+    bufs, out, k = _setup(ctx, cornell, W, H)
+    comm.shard(k)
+    d1 = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    k.set_uint(N.FRAME_COUNT, 1)
+    ctx.ExecuteKernelFrames(k, W * H, 8)
+    mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=d1)
+    assert _read(ctx, d1, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+    d1.release()
+    d2 = ctx.create_buffer(N.MEM_READ_WRITE, W * H * 16)
+    k.set_uint(N.FRAME_COUNT, 9)
+    ctx.ExecuteKernelFrames(k, W * H, 8)
+    mg.Comm.gather_bands([comm], [out], W, H, root=0, dst=d2)
+    assert _read(ctx, d2, W * H).tobytes() == _read(ctx, out, W * H).tobytes()
+    assert comm.status()["gathers"] == 2
+    comm.destroy()
+    for b in bufs + [out, d2]:
+        b.release()
+    k.release()
     ctx.release()
 
 
