@@ -135,8 +135,9 @@ struct rt_kernel_s {
     uint32_t n_nodes = 0, n_tris = 0, n_mats = 0;
     int depth = 0;
     bool last_lds = false;
-    int occ_cache[rtk::kNumSched][3][2][2][2] = {};  // [sched][math][lds][stats][bofs] -> blocks per CU (0 = unknown)
-    size_t occ_smem[rtk::kNumSched][3][2][2][2] = {};
+    // [sched][math][lds][stats][bofs or goct, + 2 for fused launches] -> blocks per CU (0 = unknown)
+    int occ_cache[rtk::kNumSched][3][2][2][4] = {};
+    size_t occ_smem[rtk::kNumSched][3][2][2][4] = {};
 };
 
 namespace {
@@ -1109,7 +1110,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
                  (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
-                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
+                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0) +
+                 (si == RT_SCHED_STEP && goct ? 4 * rtk::kDedupWaveBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end
@@ -1117,11 +1119,11 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 
     const int mi = k->math;
     const bool bofs = lds && a.octB == rtk::kOctB;
-    const int var = bofs || goct;  // occupancy cache: the variant slot
+    const int var = (bofs || goct ? 1 : 0) + (a.radBuf ? 2 : 0);  // occupancy cache: the variant slot
     int& occ = k->occ_cache[si][mi][lds][k->stats][var];
     if (occ == 0 || k->occ_smem[si][mi][lds][k->stats][var] != smem) {
         occ = wf ? rtk::occupancy_wf_extend(k->math, lds, k->stats, bofs, smem, goct)
-                 : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct);
+                 : rtk::occupancy_kernel_entry(si, k->math, lds, k->stats, bofs, smem, goct, a.radBuf != nullptr);
         k->occ_smem[si][mi][lds][k->stats][var] = smem;
     }
     uint64_t grid = (uint64_t)(k->max_blocks ? std::min(occ, k->max_blocks) : occ) * (uint64_t)ctx->num_cus;

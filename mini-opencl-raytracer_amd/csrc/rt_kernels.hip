@@ -11,24 +11,28 @@ namespace rtk {
 // 6 waves per SIMD measured 7 % faster than the 4 its natural 113 VGPRs allow
 // (profiles/r01/occupancy_ab.txt); the fp64-heavy pinned body stays at its natural budget.
 // (LDS scenes 5 waves per SIMD, scenes read from HBM/L2 6, as for the shipped policy)
-template <bool kStats, bool kBofs>
+template <bool kStats, bool kBofs, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
 void kernel_entry_step_devicelib_lds(KernelArgs a) {
-    step_body<MathDeviceLib, true, kStats, kBofs>(a);
+    step_body<MathDeviceLib, true, kStats, kBofs, false, kMode>(a);
 }
-template <bool kStats>
+template <bool kStats, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
 void kernel_entry_step_devicelib_global(KernelArgs a) {
-    step_body<MathDeviceLib, false, kStats>(a);
+    step_body<MathDeviceLib, false, kStats, false, false, kMode>(a);
 }
-template <bool kStats>
+template <bool kStats, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOCT_WAVES, 8)))
 void kernel_entry_step_devicelib_goct(KernelArgs a) {
-    step_body<MathDeviceLib, true, kStats, false, true>(a);
+    step_body<MathDeviceLib, true, kStats, false, true, kMode>(a);
 }
-template <bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct = false>
-__global__ __launch_bounds__(256) void kernel_entry_step_pinned(KernelArgs a) {
-    step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct>(a);
+#ifndef RT_STEP_PINNED_WAVES
+#define RT_STEP_PINNED_WAVES 1  // (1: no register cap -- the natural budget)
+#endif
+template <bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct, int kMode>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
+void kernel_entry_step_pinned(KernelArgs a) {
+    step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct, kMode>(a);
 }
 
 
@@ -67,34 +71,42 @@ namespace rtk {
 
 // Kernel variants: [schedule][math][scene in LDS][stats].
 
+template <class M, bool L, bool S, int kMode>
+static KernelFn pick_step(bool bofs, bool goct) {
+    if (M::kId == MathDeviceLib::kId) {
+        if (!L) return goct ? kernel_entry_step_devicelib_goct<S, kMode> : kernel_entry_step_devicelib_global<S, kMode>;
+        return bofs ? kernel_entry_step_devicelib_lds<S, true, kMode> : kernel_entry_step_devicelib_lds<S, false, kMode>;
+    }
+    if (!L) return goct ? kernel_entry_step_pinned<true, S, false, true, kMode> : kernel_entry_step_pinned<false, S, false, false, kMode>;
+    return bofs ? kernel_entry_step_pinned<true, S, true, false, kMode> : kernel_entry_step_pinned<true, S, false, false, kMode>;
+}
 template <class M, bool L, bool S>
-static KernelFn pick_sched(int sched, bool bofs, bool goct) {
+static KernelFn pick_sched(int sched, bool bofs, bool goct, bool fused) {
     if (sched == kSchedStep) {
-        if (M::kId == MathDeviceLib::kId) {
-            if (!L) return goct ? kernel_entry_step_devicelib_goct<S> : kernel_entry_step_devicelib_global<S>;
-            return bofs ? kernel_entry_step_devicelib_lds<S, true> : kernel_entry_step_devicelib_lds<S, false>;
-        }
-        if (!L) return goct ? kernel_entry_step_pinned<true, S, false, true> : kernel_entry_step_pinned<false, S, false>;
-        return bofs ? kernel_entry_step_pinned<true, S, true> : kernel_entry_step_pinned<true, S, false>;
+        if constexpr (S || !RT_SPECIALIZE_FUSED)
+            return pick_step<M, L, S, 0>(bofs, goct);
+        else
+            return fused ? pick_step<M, L, S, 1>(bofs, goct) : pick_step<M, L, S, 2>(bofs, goct);
     }
     return kernel_entry<M, L, S>;
 }
 
 // bofs: LDS node records with the B planes at kOctB (KernelArgs::octB == kOctB); goct: a scene
-// too large for LDS walked through its octant records in HBM/L2 (step schedule)
-static KernelFn pick(int sched, int math, bool lds, bool stats, bool bofs, bool goct) {
-    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats, bofs, goct);
+// too large for LDS walked through its octant records in HBM/L2 (step schedule); fused: a fused
+// frames launch (KernelArgs::radBuf set)
+static KernelFn pick(int sched, int math, bool lds, bool stats, bool bofs, bool goct, bool fused) {
+    if (math == MathShipped::kId) return pick_shipped(sched, lds, stats, bofs, goct, fused);
     if (math == MathDeviceLib::kId) {
-        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched, bofs, false) : pick_sched<MathDeviceLib, true, false>(sched, bofs, false);
-        return stats ? pick_sched<MathDeviceLib, false, true>(sched, bofs, goct) : pick_sched<MathDeviceLib, false, false>(sched, bofs, goct);
+        if (lds) return stats ? pick_sched<MathDeviceLib, true, true>(sched, bofs, false, fused) : pick_sched<MathDeviceLib, true, false>(sched, bofs, false, fused);
+        return stats ? pick_sched<MathDeviceLib, false, true>(sched, bofs, goct, fused) : pick_sched<MathDeviceLib, false, false>(sched, bofs, goct, fused);
     }
-    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched, bofs, false) : pick_sched<MathPinned, true, false>(sched, bofs, false);
-    return stats ? pick_sched<MathPinned, false, true>(sched, bofs, goct) : pick_sched<MathPinned, false, false>(sched, bofs, goct);
+    if (lds) return stats ? pick_sched<MathPinned, true, true>(sched, bofs, false, fused) : pick_sched<MathPinned, true, false>(sched, bofs, false, fused);
+    return stats ? pick_sched<MathPinned, false, true>(sched, bofs, goct, fused) : pick_sched<MathPinned, false, false>(sched, bofs, goct, fused);
 }
 
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st, bool goct) {
-    KernelFn fn = pick(sched, math, lds, stats, lds && a.octB == kOctB, goct);
+    KernelFn fn = pick(sched, math, lds, stats, lds && a.octB == kOctB, goct, a.radBuf != nullptr);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), smem, st, a);
     return hipGetLastError();
 }
@@ -121,9 +133,9 @@ hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hip
     return hipGetLastError();
 }
 
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct) {
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct, bool fused) {
     int blocks = 0;
-    KernelFn fn = pick(sched, math, lds, stats, lds && bofs, goct);
+    KernelFn fn = pick(sched, math, lds, stats, lds && bofs, goct, fused);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, smem) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
 }

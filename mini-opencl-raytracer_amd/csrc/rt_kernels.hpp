@@ -78,6 +78,13 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 // step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
 // from which its siblings take single tiles once the work counter is dry
 constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)
+// HBM/L2 octant walk (kGlobalOct, RT_GOCT_DEDUP 1): per wave, a 48-B record slot per lane into which
+// one leader lane per distinct node / triangle record of a step loads it for the others (step_body)
+#ifndef RT_GOCT_DEDUP
+#define RT_GOCT_DEDUP 0
+#endif
+constexpr uint32_t kDedupSlots = RT_GOCT_DEDUP ? 64u : 0u;
+constexpr uint32_t kDedupWaveBytes = kDedupSlots * 48u;
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address
@@ -123,7 +130,8 @@ WfKernels pick_wf_shipped(bool lds, bool stats, bool bofs, bool goct);
 // 64-B global node records
 hipError_t launch_kernel_entry(const KernelArgs& a, int sched, int math, bool lds, bool stats, unsigned grid,
                                size_t smem, hipStream_t st, bool goct = false);
-int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct = false);
+int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs, size_t smem, bool goct = false,
+                           bool fused = true);
 // accumulate the fused frames' radiances into the output (one pixel per lane)
 // (`key`: 4 words of per-kernel state for the sky shortcut, zeroed once; accum_key_body)
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st);
@@ -132,7 +140,12 @@ hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, 
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 // rt_kernels_shipped.hip: the MathShipped instantiations (own TU: OpenCL-default / and sqrt)
-KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct, bool fused);
+// the step schedule's entry points are specialised per launch kind (step_body kMode: 1 fused, 2
+// per-frame); stats builds and RT_SPECIALIZE_FUSED 0 use the generic body (kMode 0)
+#ifndef RT_SPECIALIZE_FUSED
+#define RT_SPECIALIZE_FUSED 1
+#endif
 hipError_t launch_pack_mats_shipped(const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 
 }  // namespace rtk

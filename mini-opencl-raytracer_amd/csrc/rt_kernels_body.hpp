@@ -307,6 +307,58 @@ __device__ __forceinline__ uint32_t oct_step_g(const SceneView& sc, const Kernel
     return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
 }
 
+// The same step with de-duplicated loads (RT_GOCT_DEDUP): a step's ~40 walking lanes read only ~5
+// distinct records (profiles/r05/goct_coherence_pixel_major.txt), and the vector-memory address
+// unit's cost grows with the lanes a load serves (profiles/r03/ta_width_probe.txt).  One leader lane
+// per distinct record (readlane + ballot over the distinct keys) loads it into its LDS slot of the
+// wave; every lane then reads its record from its leader's slot.  The same bits; only who loads
+// them changes.  Returns the lane's leader (the lane itself for a leader).
+__device__ __forceinline__ uint32_t dedup_leader(uint32_t key) {
+    unsigned long long rem = __ballot(true);  // the lanes running this step (their exec mask)
+    uint32_t j = 0u;
+    while (rem != 0ull) {  // wave-uniform: one round per distinct key
+        const uint32_t l = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t k = __builtin_amdgcn_readlane(key, l);
+        const bool mine = key == k;
+        rem &= ~__ballot(mine);
+        j = mine ? l : j;
+    }
+    return j;
+}
+
+template <bool kBofs>
+__device__ __forceinline__ uint32_t oct_step_gd(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
+                                                float t, uint32_t& skip, sv4f* ds) {
+    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
+    const uint32_t ob = kBofs ? kOctB : a.octB;
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i);
+    sv4f A, B;
+    if (__ballot(i != i0) == 0ull) {  // every walking lane at one record: the scalar cache
+        const cv4f* cp = (const cv4f*)sc.onodes;
+        A = cp[i0];
+        B = cp[i0 + ob];
+    } else {
+        const uint32_t j = dedup_leader(i);
+        if (j == __lane_id()) {  // (both loads in flight before either store)
+            const sv4f la = *reinterpret_cast<const sv4f*>(sc.onodes + i);
+            const sv4f lb = *reinterpret_cast<const sv4f*>(sc.onodes + i + ob);
+            ds[3u * j] = la;
+            ds[3u * j + 1u] = lb;
+        }
+        __builtin_amdgcn_wave_barrier();
+        A = ds[3u * j];
+        B = ds[3u * j + 1u];
+    }
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    skip = __float_as_uint(B.w);
+    return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
+}
+
 // kernel_bvh.cl:98-153 (RayTriangle), accept test only.  Branch-free: the reference's
 // early returns (det, u, v) become one accept predicate (ray_triangle below).  The values computed are the
 // ones the reference computes where it reaches them; the rest are discarded.  A wave
@@ -339,6 +391,35 @@ __device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
 
 // the same on a scene read from HBM/L2 (oct_step_g): through the scalar cache when every testing
 // lane is at one triangle
+// tri_eval_g with de-duplicated loads (oct_step_gd)
+template <class M>
+__device__ __forceinline__ TriEval tri_eval_gd(const float4* tris, uint32_t idx, const Ray& r, sv4f* ds) {
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(idx);
+    sv4f va, vb;
+    float vc;
+    if (__ballot(idx != i0) == 0ull) {  // every testing lane at one triangle
+        const cv4f* cp = (const cv4f*)tris;
+        va = cp[3u * i0];
+        vb = cp[3u * i0 + 1u];
+        vc = *((cf32*)(tris + 3u * i0 + 2u));
+    } else {
+        const uint32_t j = dedup_leader(idx);
+        if (j == __lane_id()) {  // (all three loads in flight before any store)
+            const sv4f la = *reinterpret_cast<const sv4f*>(tris + 3u * idx);
+            const sv4f lb = *reinterpret_cast<const sv4f*>(tris + 3u * idx + 1u);
+            const float lc = *reinterpret_cast<const float*>(tris + 3u * idx + 2u);
+            ds[3u * j] = la;
+            ds[3u * j + 1u] = lb;
+            reinterpret_cast<float*>(ds + 3u * j + 2u)[0] = lc;
+        }
+        __builtin_amdgcn_wave_barrier();
+        va = ds[3u * j];
+        vb = ds[3u * j + 1u];
+        vc = reinterpret_cast<const float*>(ds + 3u * j + 2u)[0];
+    }
+    return tri_eval_v<M>(va, vb, vc, r);
+}
+
 template <class M>
 __device__ __forceinline__ TriEval tri_eval_g(const float4* tris, uint32_t idx, const Ray& r) {
     const uint32_t i0 = __builtin_amdgcn_readfirstlane(idx);
@@ -768,6 +849,9 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_NODE_BURST
 #define RT_NODE_BURST 7  // LDS walk (6 before work stealing; 5 / 8 slower: profiles/r03/burst_sweep.txt)
 #endif
+#ifndef RT_BURST_ADAPT
+#define RT_BURST_ADAPT 0
+#endif
 // diagnostic (stats variant, scripts/timeline.py): wave start/end timeline instead of the
 // lane-wait counters
 #ifndef RT_TIMELINE
@@ -896,7 +980,11 @@ __device__ __forceinline__ bool take_tile(const KernelArgs& a, unsigned long lon
     return false;
 }
 
-template <class M, bool kLdsScene, bool kStats, bool kBofs = false, bool kGlobalOct = false>
+// kMode: 0 -- one body for both launch kinds (fused frames when a.radBuf is set); 1 -- fused
+// launches only (rtEnqueueKernelFrames); 2 -- per-frame launches only.  The specialised bodies
+// leave out the other kind's code (finish queue, sky key, frame slots), which otherwise holds
+// registers in the hot loop (52 SGPRs spilled to VGPR lanes in the generic body).
+template <class M, bool kLdsScene, bool kStats, bool kBofs = false, bool kGlobalOct = false, int kMode = 0>
 __device__ __forceinline__ void step_body(const KernelArgs& a) {
     const int tid = threadIdx.x;
     // scenes read from HBM/L2: the render's waves issue ahead of co-resident accumulation waves
@@ -906,7 +994,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // frames fused into this launch (rtEnqueueKernelFrames): work item = (frame slot, pixel);
     // a finished path stores its radiance in radBuf[slot][gid] for accum_frames, and the lane's
     // `gid` register then holds slot * radStride + gid
-    const bool fused = a.radBuf != nullptr;
+    const bool fused = kMode == 1 ? true : kMode == 2 ? false : a.radBuf != nullptr;
     // the waves' remaining chunks (work stealing, take_tile): empty ranges before anyone looks
     unsigned long long* steal = nullptr;
     {
@@ -917,6 +1005,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             (kRingLds ? 4u * (fused ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u) : 0u));
         if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
     }
+    // HBM/L2 octant walk: this wave's de-duplicated record slots (RT_GOCT_DEDUP), after the steal words
+    [[maybe_unused]] sv4f* dds = reinterpret_cast<sv4f*>(steal) + kStealBytes / 16u + (uint32_t)(tid >> 6) * (kDedupWaveBytes / 16u);
     const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
     if (kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
 
@@ -1350,9 +1440,19 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #endif
                         if (cur < kLeafMin) {
                             if (kStats && cur != a.nNodes) ++st.visits;
-                            cur = kGlobalOct ? oct_step_g<kBofs>(sc, a, cur, ray, h.t, leaf_i)
-                                             : oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
+                            if constexpr (kGlobalOct && kDedupSlots > 0)
+                                cur = oct_step_gd<kBofs>(sc, a, cur, ray, h.t, leaf_i, dds);
+                            else
+                                cur = kGlobalOct ? oct_step_g<kBofs>(sc, a, cur, ray, h.t, leaf_i)
+                                                 : oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
                         }
+#if RT_BURST_ADAPT
+                        // (diagnostic variant) end the burst early once fewer than
+                        // RT_BURST_ADAPT / 16 of the decision's walking lanes still walk
+                        if (!kGlobalOct && rep >= 2 && rep + 1 < kNodeBurst &&
+                            popc_ballot(cur < a.nNodes) * 16u < n_trav * (uint32_t)RT_BURST_ADAPT)
+                            break;
+#endif
                     } else if (state == kTrav) {
                         if (kStats) ++st.visits;
                         uint32_t next, first = 0, count = 0;
@@ -1399,7 +1499,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if ((int32_t)cur >= (int32_t)kLeafMin) {
                             if (kStats) ++st.tests;
                             const uint32_t idx = cur & 0x00ffffffu;
-                            if (kGlobalOct)
+                            if constexpr (kGlobalOct && kDedupSlots > 0)
+                                tri_accept(tri_eval_gd<M>(sc.tris, idx, ray, dds), (int32_t)idx, h);
+                            else if (kGlobalOct)
                                 tri_accept(tri_eval_g<M>(sc.tris, idx, ray), (int32_t)idx, h);
                             else
                                 ray_triangle<M>(sc.tris + 3 * idx, (int32_t)idx, ray, h);

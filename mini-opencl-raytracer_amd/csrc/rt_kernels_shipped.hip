@@ -14,21 +14,21 @@ namespace rtk {
 
 // LDS-resident scenes run 5 waves per SIMD (VALU-bound); scenes read from HBM/L2 run 6 (load
 // latency to hide: bunny proxy -2.4 %, profiles/r01/global_path_waves_ab.txt)
-template <bool kStats, bool kBofs>
+template <bool kStats, bool kBofs, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_DEVICELIB_WAVES, 8)))
 void kernel_entry_step_shipped_lds(KernelArgs a) {
-    step_body<MathShipped, true, kStats, kBofs>(a);
+    step_body<MathShipped, true, kStats, kBofs, false, kMode>(a);
 }
-template <bool kStats>
+template <bool kStats, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GLOBAL_WAVES, 8)))
 void kernel_entry_step_shipped_global(KernelArgs a) {
-    step_body<MathShipped, false, kStats>(a);
+    step_body<MathShipped, false, kStats, false, false, kMode>(a);
 }
 // octant records read from HBM/L2 (scenes too large for LDS): the LDS path's walk
-template <bool kStats>
+template <bool kStats, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOCT_WAVES, 8)))
 void kernel_entry_step_shipped_goct(KernelArgs a) {
-    step_body<MathShipped, true, kStats, false, true>(a);
+    step_body<MathShipped, true, kStats, false, true, kMode>(a);
 }
 
 __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4* __restrict__ out, uint32_t n) {
@@ -37,18 +37,28 @@ __global__ void pack_mats_shipped(const rt_cl_material* __restrict__ in, float4*
     material_record<MathShipped>(in[i], out + 4 * i);
 }
 
+template <bool L, bool S, int kMode>
+static KernelFn pick_step_shipped(bool bofs, bool goct) {
+    if (!L) return goct ? kernel_entry_step_shipped_goct<S, kMode> : kernel_entry_step_shipped_global<S, kMode>;
+    return bofs ? kernel_entry_step_shipped_lds<S, true, kMode> : kernel_entry_step_shipped_lds<S, false, kMode>;
+}
 template <bool L, bool S>
-static KernelFn pick_sched_shipped(int sched, bool bofs, bool goct) {
+static KernelFn pick_sched_shipped(int sched, bool bofs, bool goct, bool fused) {
     if (sched == kSchedStep) {
-        if (!L) return goct ? kernel_entry_step_shipped_goct<S> : kernel_entry_step_shipped_global<S>;
-        return bofs ? kernel_entry_step_shipped_lds<S, true> : kernel_entry_step_shipped_lds<S, false>;
+        if constexpr (S || !RT_SPECIALIZE_FUSED)
+            return pick_step_shipped<L, S, 0>(bofs, goct);
+        else
+            return fused ? pick_step_shipped<L, S, 1>(bofs, goct) : pick_step_shipped<L, S, 2>(bofs, goct);
     }
     return kernel_entry<MathShipped, L, S>;
 }
 
-KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct) {
-    if (lds) return stats ? pick_sched_shipped<true, true>(sched, bofs, false) : pick_sched_shipped<true, false>(sched, bofs, false);
-    return stats ? pick_sched_shipped<false, true>(sched, bofs, goct) : pick_sched_shipped<false, false>(sched, bofs, goct);
+KernelFn pick_shipped(int sched, bool lds, bool stats, bool bofs, bool goct, bool fused) {
+    if (lds)
+        return stats ? pick_sched_shipped<true, true>(sched, bofs, false, fused)
+                     : pick_sched_shipped<true, false>(sched, bofs, false, fused);
+    return stats ? pick_sched_shipped<false, true>(sched, bofs, goct, fused)
+                 : pick_sched_shipped<false, false>(sched, bofs, goct, fused);
 }
 
 __global__ __launch_bounds__(256) RT_ACCUM_OCC void accum_frames_shipped(KernelArgs a, const uint32_t* key) {

@@ -46,27 +46,61 @@ __device__ __forceinline__ F3 operator/(F3 a, float s) { return F3{a.x / s, a.y 
 __device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
 
 // ---------------------------------------------------------------------------------------
+// RT_PINNED_DIAG_* (diagnostic variant builds only, scripts/build_variant.sh): swap one pinned
+// operation for the hardware / device-library form to price it -- NOT bit-exact, never shipped
+#ifndef RT_PINNED_DIAG_DIV
+#define RT_PINNED_DIAG_DIV 0
+#endif
+#ifndef RT_PINNED_DIAG_SQRT
+#define RT_PINNED_DIAG_SQRT 0
+#endif
+#ifndef RT_PINNED_DIAG_POW
+#define RT_PINNED_DIAG_POW 0
+#endif
+#ifndef RT_PINNED_DIAG_TRIG
+#define RT_PINNED_DIAG_TRIG 0
+#endif
 struct MathPinned {
     static constexpr int kId = 0;
     static constexpr bool kContract = false;
     // the reference's `/` and sqrt: IEEE, correctly rounded
+#if RT_PINNED_DIAG_DIV
+    __device__ __forceinline__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+    __device__ __forceinline__ static float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+#else
     __device__ __forceinline__ static float rcp(float x) { return 1.0f / x; }
     __device__ __forceinline__ static float div(float a, float b) { return a / b; }
+#endif
+#if RT_PINNED_DIAG_SQRT
+    __device__ __forceinline__ static float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+    __device__ __forceinline__ static float rsqrt(float d) { return __builtin_amdgcn_rsqf(d); }
+#else
     __device__ __forceinline__ static float sqrt(float x) { return __builtin_sqrtf(x); }
+    __device__ __forceinline__ static float rsqrt(float d) { return pm_rsqrt(d); }
+#endif
     __device__ __forceinline__ static float dot(F3 a, F3 b) {
         return (a.x * b.x + a.y * b.y) + a.z * b.z;
     }
     __device__ __forceinline__ static F3 cross(F3 a, F3 b) {
         return F3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
     }
-    __device__ __forceinline__ static float rsqrt(float d) { return pm_rsqrt(d); }
+#if RT_PINNED_DIAG_POW
+    __device__ __forceinline__ static float pow(float x, float y) { return ::powf(x, y); }
+#else
     __device__ __forceinline__ static float pow(float x, float y) { return pm_pow(x, y); }
+#endif
     // pow(x, 2.0f) call sites of the reference (kernel_bvh.cl:224, :275): pinned as the
     // exact square, as LLVM's libcall simplifiers fold it (rt_pinned_math.h)
     __device__ __forceinline__ static float pow2(float x) { return pm_sq(x); }
+#if RT_PINNED_DIAG_TRIG
+    __device__ __forceinline__ static float sin(float x) { return ::sinf(x); }
+    __device__ __forceinline__ static float cos(float x) { return ::cosf(x); }
+    __device__ __forceinline__ static void sincos(float x, float& s, float& c) { ::sincosf(x, &s, &c); }
+#else
     __device__ __forceinline__ static float sin(float x) { return pm_sin(x); }
     __device__ __forceinline__ static float cos(float x) { return pm_cos(x); }
     __device__ __forceinline__ static void sincos(float x, float& s, float& c) { pm_sincos(x, &s, &c); }
+#endif
     __device__ __forceinline__ static float tan(float x) { return pm_tan(x); }
     __device__ __forceinline__ static float max(float x, float y) { return pm_max(x, y); }
     __device__ __forceinline__ static float min(float x, float y) { return pm_min(x, y); }
