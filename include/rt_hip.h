@@ -490,6 +490,18 @@ typedef struct rt_rect {
 int rtBandPackPlan(unsigned width, unsigned height, unsigned period, unsigned phase, rt_rect* rects,
                    int capacity, int* n_rects, size_t* staging_bytes);
 
+/* The pinned math policy's builtins evaluated on the GPU, element-wise over n host values (for
+ * tests: the same device functions the pinned KernelEntry runs).  op: RT_PINNED_OP_*; b is read
+ * by the two-operand ops only.  Blocking. */
+#define RT_PINNED_OP_RCP 0    /* 1.0f / a  (correctly rounded) */
+#define RT_PINNED_OP_DIV 1    /* a / b     (correctly rounded) */
+#define RT_PINNED_OP_SQRT 2   /* sqrt(a)   (correctly rounded) */
+#define RT_PINNED_OP_RSQRT 3  /* 1.0f / sqrt(a), two rounded operations (normalize's, a >= 2^-126) */
+#define RT_PINNED_OP_POW 4    /* pow(a, b) (rt_pinned_math.h pm_pow) */
+#define RT_PINNED_OP_SIN 5
+#define RT_PINNED_OP_COS 6
+int rtDiagPinnedMath(int device_index, int op, const float* a, const float* b, float* out, size_t n);
+
 /* Library identification (for smoke checks): returns a static string. */
 const char* rtGetBuildInfo(void);
 

@@ -181,6 +181,7 @@ _HIP_PROTOS = {
     "rtBandPackPlan": (ctypes.c_int, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(Rect),
                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)]),
     "rtGetBuildInfo": (ctypes.c_char_p, []),
+    "rtDiagPinnedMath": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_size_t]),
 }
 HIP_EXPORTS = tuple(_HIP_PROTOS)
 
@@ -235,3 +236,18 @@ def hip_lib() -> ctypes.CDLL:
 def scene_lib() -> ctypes.CDLL:
     """librt_scene.so -- the host scene pipeline."""
     return _load(SCENE_LIB_PATH, _SCENE_PROTOS)
+
+
+PINNED_OPS = {"rcp": 0, "div": 1, "sqrt": 2, "rsqrt": 3, "pow": 4, "sin": 5, "cos": 6}
+
+
+def pinned_math(op: str, a, b=None, device: int = 0) -> np.ndarray:
+    """rtDiagPinnedMath: the pinned policy's device builtins, element-wise (tests)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    bb = None if b is None else np.ascontiguousarray(np.broadcast_to(np.float32(b) if np.isscalar(b) else b, a.shape),
+                                                     dtype=np.float32)
+    out = np.empty_like(a)
+    check(hip_lib().rtDiagPinnedMath(int(device), PINNED_OPS[op], a.ctypes.data,
+                                     None if bb is None else bb.ctypes.data, out.ctypes.data, a.size),
+          f"pinned math {op}")
+    return out

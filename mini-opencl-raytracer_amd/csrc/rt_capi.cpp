@@ -1053,7 +1053,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
             // (buffer writes, per-frame launches) but not after the previous step's render or
             // accumulation: it fills the CUs that render's draining waves free.  (With hit
             // buffers bound the renders stay in order on the main stream: each writes them.)
-            rstr = ctx->rstream[rs];
+            rstr = ctx->rstream[ctx->rnext];
+            ctx->rnext = (ctx->rnext + 1) % RT_RENDER_STREAMS;
             hipError_t me = rti::main_tail_wait(ctx, rstr);
             if (me != hipSuccess) return map_hip(me);
         }
@@ -1110,8 +1111,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
            : (lds ? scene_bytes : (size_t)a.nTop * 64) +
                  (si == RT_SCHED_STEP && !fused ? 4 * rtk::kFinishWaveBytes : 0) +
                  (si == RT_SCHED_STEP && lds ? 4 * (fused ? rtk::kRingWaveBytes : rtk::kRingWaveBytesPf) : 0) +
-                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0) +
-                 (si == RT_SCHED_STEP && goct ? 4 * rtk::kDedupWaveBytes : 0);
+                 (si == RT_SCHED_STEP ? rtk::kStealBytes : 0);
     k->last_lds = lds;
     // the step schedule's ray ring (LDS scenes) writes each tile's frame flags as one word at ring
     // fill; the other fused renders write a byte per path at its end
@@ -1720,6 +1720,27 @@ int rtContextSetAccumOverlap(rt_context ctx, int enable) {
     if (e != hipSuccess) return map_hip(e);
     ctx->overlap = enable != 0;
     return RT_SUCCESS;
+}
+
+int rtDiagPinnedMath(int device_index, int op, const float* a, const float* b, float* out, size_t n) {
+    if (op < RT_PINNED_OP_RCP || op > RT_PINNED_OP_COS || !a || !out) return RT_INVALID_VALUE;
+    const bool two = op == RT_PINNED_OP_DIV || op == RT_PINNED_OP_POW;
+    if (two && !b) return RT_INVALID_VALUE;
+    if (n == 0) return RT_SUCCESS;
+    if (n > ((size_t)1 << 28)) return RT_INVALID_BUFFER_SIZE;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return RT_DEVICE_NOT_FOUND;
+    if (device_index < 0 || device_index >= count) return RT_INVALID_DEVICE;
+    hipError_t e = hipSetDevice(device_index);
+    float* d = nullptr;
+    const size_t bytes = n * sizeof(float);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d), 3 * bytes);
+    if (e == hipSuccess) e = hipMemcpy(d, a, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && two) e = hipMemcpy(d + n, b, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtk::launch_pinned_math(op, d, d + n, d + 2 * n, n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, bytes, hipMemcpyDeviceToHost);
+    if (d) (void)hipFree(d);
+    return map_hip(e);
 }
 
 const char* rtGetBuildInfo(void) {

@@ -10,10 +10,14 @@
 
 #include "../../include/rt_hip.h"
 
-// fused frames: radiance sets (and render streams) used in rotation, so a render waits only for
-// the accumulation of the launch RT_RAD_SETS steps back
+// fused frames: radiance sets used in rotation, so a render waits only for the accumulation of the
+// launch RT_RAD_SETS steps back; consecutive renders alternate between RT_RENDER_STREAMS streams, so
+// at most that many renders are in flight
 #ifndef RT_RAD_SETS
 #define RT_RAD_SETS 2
+#endif
+#ifndef RT_RENDER_STREAMS
+#define RT_RENDER_STREAMS 2
 #endif
 
 struct rt_context_s {
@@ -30,7 +34,8 @@ struct rt_context_s {
     // fused renders alternate between two streams, one per radiance set (rt_capi.cpp enqueue):
     // renders of consecutive steps are independent, so step k+1's waves take the CUs that step
     // k's draining waves free instead of waiting for its last path
-    hipStream_t rstream[RT_RAD_SETS] = {};
+    hipStream_t rstream[RT_RENDER_STREAMS] = {};
+    int rnext = 0;  // the render stream of the next fused render
     hipEvent_t mtail = nullptr;  // main stream's tail, for copies issued on astream
     // Work may have been enqueued on the main stream since mtail was last recorded
     // (main_tail_wait).  Streams share hardware queues (GPU_MAX_HW_QUEUES 4 < the context's and

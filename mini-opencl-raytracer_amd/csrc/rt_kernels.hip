@@ -26,11 +26,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_GOC
 void kernel_entry_step_devicelib_goct(KernelArgs a) {
     step_body<MathDeviceLib, true, kStats, false, true, kMode>(a);
 }
+// The pinned body on LDS scenes: 5 waves per SIMD (96 VGPRs, 80 B of spills) against the 4 its
+// natural 116 VGPRs allow -- 4K Cornell 8 spp 1.044 -> 1.007 ms/frame (profiles/r06/pinned_ab.txt);
+// the HBM/L2 walks keep their natural budget (1: no register cap)
 #ifndef RT_STEP_PINNED_WAVES
-#define RT_STEP_PINNED_WAVES 1  // (1: no register cap -- the natural budget)
+#define RT_STEP_PINNED_WAVES 5
 #endif
 template <bool kLdsScene, bool kStats, bool kBofs, bool kGlobalOct, int kMode>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_PINNED_WAVES, 8)))
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(kLdsScene && !kGlobalOct ? RT_STEP_PINNED_WAVES : 1, 8)))
 void kernel_entry_step_pinned(KernelArgs a) {
     step_body<MathPinned, kLdsScene, kStats, kBofs, kGlobalOct, kMode>(a);
 }
@@ -176,6 +180,30 @@ int occupancy_wf_shade(int math, bool stats) {
     const WfKernels kf = pick_wf(math, false, stats, false, false);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kf.shade, kWfShadeThreads, 0) != hipSuccess) return 1;
     return blocks > 0 ? blocks : 1;
+}
+
+// rtDiagPinnedMath: the pinned policy's builtins, element-wise (tests)
+__global__ void pinned_math_kernel(int op, const float* __restrict__ a, const float* __restrict__ b,
+                                   float* __restrict__ out, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i];
+    float r;
+    switch (op) {
+        case 0: r = MathPinned::rcp(x); break;
+        case 1: r = MathPinned::div(x, b[i]); break;
+        case 2: r = MathPinned::sqrt(x); break;
+        case 3: r = MathPinned::rsqrt(x); break;
+        case 4: r = MathPinned::pow(x, b[i]); break;
+        case 5: r = MathPinned::sin(x); break;
+        default: r = MathPinned::cos(x); break;
+    }
+    out[i] = r;
+}
+
+hipError_t launch_pinned_math(int op, const float* a, const float* b, float* out, size_t n, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(pinned_math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, op, a, b, out, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,

@@ -78,13 +78,6 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 // step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
 // from which its siblings take single tiles once the work counter is dry
 constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)
-// HBM/L2 octant walk (kGlobalOct, RT_GOCT_DEDUP 1): per wave, a 48-B record slot per lane into which
-// one leader lane per distinct node / triangle record of a step loads it for the others (step_body)
-#ifndef RT_GOCT_DEDUP
-#define RT_GOCT_DEDUP 0
-#endif
-constexpr uint32_t kDedupSlots = RT_GOCT_DEDUP ? 64u : 0u;
-constexpr uint32_t kDedupWaveBytes = kDedupSlots * 48u;
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address
@@ -136,6 +129,7 @@ int occupancy_kernel_entry(int sched, int math, bool lds, bool stats, bool bofs,
 // (`key`: 4 words of per-kernel state for the sky shortcut, zeroed once; accum_key_body)
 hipError_t launch_accum_frames(const KernelArgs& a, int math, uint32_t* key, hipStream_t st);
 hipError_t launch_accum_frames_shipped(const KernelArgs& a, uint32_t* key, hipStream_t st);
+hipError_t launch_pinned_math(int op, const float* a, const float* b, float* out, size_t n, hipStream_t st);
 hipError_t launch_pack(const rt_cl_triangle* tris, uint32_t n_tris, float4* pt, float4* ps,
                        const rt_cl_material* mats, uint32_t n_mats, float4* pm, hipStream_t st);
 

@@ -158,6 +158,47 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
     return SceneView{a.gNodes, a.packedTris, smem, a.shadeTris, a.shadeMats};
 }
 
+// The step schedule's LDS walk (RT_WALK_ADDR): the octant records staged with their successor words
+// turned into LDS byte addresses -- a node word becomes the byte address of the A record of the same
+// octant, a leaf code count << 24 | first becomes count << 24 | the byte address of triangle `first`'s
+// record, END (each octant's sentinel) kEndWalk, a word that is neither (a walk that reaches it leaves
+// the node and triangle steps at once, and is ready to shade: no sentinel visits, no END test per
+// decision).  A visit reads its records at the word itself and a triangle step at the leaf word's low
+// bits: no address arithmetic on the dependent path (one VALU per node visit).  The dynamic LDS
+// of these kernels starts at LDS address 0 (no static __shared__), so a byte address is a byte
+// offset into smem.
+#ifndef RT_WALK_ADDR
+#define RT_WALK_ADDR 1
+#endif
+constexpr uint32_t kEndWalk = 0xff000000u;  // END as a byte-address walk word: neither a node nor a leaf
+__device__ __forceinline__ uint32_t walk_word(uint32_t w, uint32_t octant, const KernelArgs& a) {
+    if (w >= kLeafMin) return (w & 0xff000000u) | (a.octRecords * 16u + (w & 0x00ffffffu) * 48u);
+    if (w >= a.nNodes) return kEndWalk;
+    return (octant * a.octStride + w) * 16u;
+}
+__device__ __forceinline__ SceneView stage_scene_walk(const KernelArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int tid = threadIdx.x;
+    float4* lo = smem;
+    float4* lt = lo + a.octRecords;
+    float4* ls = lt + 3 * a.nTris;
+    float4* lm = ls + 3 * a.nTris;
+    for (uint32_t i = tid; i < a.octRecords; i += 256) {
+        float4 r = a.octNodes[i];
+        if (i >= a.octB && i < a.octB + 8u * a.octStride) {  // a B record: {far.yz, hit_next, miss_next}
+            const uint32_t o = (i - a.octB) / a.octStride;
+            r.z = __uint_as_float(walk_word(__float_as_uint(r.z), o, a));
+            r.w = __uint_as_float(walk_word(__float_as_uint(r.w), o, a));
+        }
+        lo[i] = r;
+    }
+    for (uint32_t i = tid; i < 3 * a.nTris; i += 256) lt[i] = a.packedTris[i];
+    for (uint32_t i = tid; i < 3 * a.nTris; i += 256) ls[i] = a.shadeTris[i];
+    for (uint32_t i = tid; i < 4 * a.nMats; i += 256) lm[i] = a.shadeMats[i];
+    __syncthreads();
+    return SceneView{nullptr, lt, lo, ls, lm};
+}
+
 // LDS float4s of the scene (the finish queue / pool follow it)
 template <bool kLdsScene, bool kGlobalOct = false>
 __device__ __forceinline__ uint32_t lds_scene_f4(const KernelArgs& a) {
@@ -270,6 +311,9 @@ __device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelAr
     return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
 }
 
+// (De-duplicated loads -- one leader lane per distinct record loads it into LDS for the others --
+// cut the address unit's busy share 0.835 -> 0.516 but cost 57 % more VALU and an LDS round trip
+// per step: bunny proxy 1.24 -> 2.19 ms/frame, profiles/r06/goct_dedup_ab.txt; removed.)
 // Scenes read from HBM/L2 (the octant walk over global records): a node or triangle step's loads
 // are the work the vector-memory address unit is bound by (bunny proxy: `ta_busy` 0.91).  A step's
 // ~40 walking lanes read only ~5 distinct records (camera rays of a tile and its frames walk
@@ -279,6 +323,31 @@ __device__ __forceinline__ uint32_t oct_step(const SceneView& sc, const KernelAr
 // lane's record through the scalar cache in every step, the other lanes' by vector loads, cut the
 // address unit's wavefronts by 10 % but put the scalar cache's latency on every step: +15 %.)
 typedef float sv4f __attribute__((ext_vector_type(4)));
+// records at an LDS byte address (the LDS walk's words; the pointer in LDS's own address space, so a
+// ds_read at the address itself): a node's A / B record, a triangle's two 16-B reads and one 4-B read
+__device__ __forceinline__ sv4f lds_v4_at(uint32_t byte_addr) {
+    return *reinterpret_cast<__attribute__((address_space(3))) const sv4f*>((size_t)byte_addr);
+}
+__device__ __forceinline__ float lds_f32_at(uint32_t byte_addr) {
+    return *reinterpret_cast<__attribute__((address_space(3))) const float*>((size_t)byte_addr);
+}
+
+// oct_step on byte-address walk words (stage_scene_walk): `cur` is the A record's LDS byte address
+template <bool kBofs>
+__device__ __forceinline__ uint32_t oct_step_w(const KernelArgs& a, uint32_t cur, const Ray& r, float t,
+                                               uint32_t& skip) {
+    const sv4f A = lds_v4_at(cur);
+    const sv4f B = lds_v4_at(cur + 16u * (kBofs ? kOctB : a.octB));
+    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
+    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
+    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
+    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
+    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
+    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
+    skip = __float_as_uint(B.w);
+    return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
+}
+
 typedef __attribute__((address_space(4))) const sv4f cv4f;
 typedef __attribute__((address_space(4))) const float cf32;
 
@@ -296,58 +365,6 @@ __device__ __forceinline__ uint32_t oct_step_g(const SceneView& sc, const Kernel
     } else {
         A = *reinterpret_cast<const sv4f*>(sc.onodes + i);
         B = *reinterpret_cast<const sv4f*>(sc.onodes + i + ob);
-    }
-    float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
-    float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
-    t0 = __builtin_fmaxf(t0, (A.y - r.o.y) * r.inv.y);
-    t1 = __builtin_fminf(t1, (B.x - r.o.y) * r.inv.y);
-    t0 = __builtin_fmaxf(t0, (A.z - r.o.z) * r.inv.z);
-    t1 = __builtin_fminf(t1, (B.y - r.o.z) * r.inv.z);
-    skip = __float_as_uint(B.w);
-    return t1 >= t0 ? __float_as_uint(B.z) : __float_as_uint(B.w);
-}
-
-// The same step with de-duplicated loads (RT_GOCT_DEDUP): a step's ~40 walking lanes read only ~5
-// distinct records (profiles/r05/goct_coherence_pixel_major.txt), and the vector-memory address
-// unit's cost grows with the lanes a load serves (profiles/r03/ta_width_probe.txt).  One leader lane
-// per distinct record (readlane + ballot over the distinct keys) loads it into its LDS slot of the
-// wave; every lane then reads its record from its leader's slot.  The same bits; only who loads
-// them changes.  Returns the lane's leader (the lane itself for a leader).
-__device__ __forceinline__ uint32_t dedup_leader(uint32_t key) {
-    unsigned long long rem = __ballot(true);  // the lanes running this step (their exec mask)
-    uint32_t j = 0u;
-    while (rem != 0ull) {  // wave-uniform: one round per distinct key
-        const uint32_t l = (uint32_t)__builtin_ctzll(rem);
-        const uint32_t k = __builtin_amdgcn_readlane(key, l);
-        const bool mine = key == k;
-        rem &= ~__ballot(mine);
-        j = mine ? l : j;
-    }
-    return j;
-}
-
-template <bool kBofs>
-__device__ __forceinline__ uint32_t oct_step_gd(const SceneView& sc, const KernelArgs& a, uint32_t cur, const Ray& r,
-                                                float t, uint32_t& skip, sv4f* ds) {
-    const uint32_t i = __umul24(r.sgn, a.octStride) + cur;
-    const uint32_t ob = kBofs ? kOctB : a.octB;
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i);
-    sv4f A, B;
-    if (__ballot(i != i0) == 0ull) {  // every walking lane at one record: the scalar cache
-        const cv4f* cp = (const cv4f*)sc.onodes;
-        A = cp[i0];
-        B = cp[i0 + ob];
-    } else {
-        const uint32_t j = dedup_leader(i);
-        if (j == __lane_id()) {  // (both loads in flight before either store)
-            const sv4f la = *reinterpret_cast<const sv4f*>(sc.onodes + i);
-            const sv4f lb = *reinterpret_cast<const sv4f*>(sc.onodes + i + ob);
-            ds[3u * j] = la;
-            ds[3u * j + 1u] = lb;
-        }
-        __builtin_amdgcn_wave_barrier();
-        A = ds[3u * j];
-        B = ds[3u * j + 1u];
     }
     float t0 = __builtin_fmaxf(0.0f, (A.x - r.o.x) * r.inv.x);
     float t1 = __builtin_fminf(t, (A.w - r.o.x) * r.inv.x);
@@ -391,35 +408,6 @@ __device__ __forceinline__ TriEval tri_eval(const float4* tri, const Ray& r) {
 
 // the same on a scene read from HBM/L2 (oct_step_g): through the scalar cache when every testing
 // lane is at one triangle
-// tri_eval_g with de-duplicated loads (oct_step_gd)
-template <class M>
-__device__ __forceinline__ TriEval tri_eval_gd(const float4* tris, uint32_t idx, const Ray& r, sv4f* ds) {
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane(idx);
-    sv4f va, vb;
-    float vc;
-    if (__ballot(idx != i0) == 0ull) {  // every testing lane at one triangle
-        const cv4f* cp = (const cv4f*)tris;
-        va = cp[3u * i0];
-        vb = cp[3u * i0 + 1u];
-        vc = *((cf32*)(tris + 3u * i0 + 2u));
-    } else {
-        const uint32_t j = dedup_leader(idx);
-        if (j == __lane_id()) {  // (all three loads in flight before any store)
-            const sv4f la = *reinterpret_cast<const sv4f*>(tris + 3u * idx);
-            const sv4f lb = *reinterpret_cast<const sv4f*>(tris + 3u * idx + 1u);
-            const float lc = *reinterpret_cast<const float*>(tris + 3u * idx + 2u);
-            ds[3u * j] = la;
-            ds[3u * j + 1u] = lb;
-            reinterpret_cast<float*>(ds + 3u * j + 2u)[0] = lc;
-        }
-        __builtin_amdgcn_wave_barrier();
-        va = ds[3u * j];
-        vb = ds[3u * j + 1u];
-        vc = reinterpret_cast<const float*>(ds + 3u * j + 2u)[0];
-    }
-    return tri_eval_v<M>(va, vb, vc, r);
-}
-
 template <class M>
 __device__ __forceinline__ TriEval tri_eval_g(const float4* tris, uint32_t idx, const Ray& r) {
     const uint32_t i0 = __builtin_amdgcn_readfirstlane(idx);
@@ -849,9 +837,6 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 #ifndef RT_NODE_BURST
 #define RT_NODE_BURST 7  // LDS walk (6 before work stealing; 5 / 8 slower: profiles/r03/burst_sweep.txt)
 #endif
-#ifndef RT_BURST_ADAPT
-#define RT_BURST_ADAPT 0
-#endif
 // diagnostic (stats variant, scripts/timeline.py): wave start/end timeline instead of the
 // lane-wait counters
 #ifndef RT_TIMELINE
@@ -1005,9 +990,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             (kRingLds ? 4u * (fused ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u) : 0u));
         if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
     }
-    // HBM/L2 octant walk: this wave's de-duplicated record slots (RT_GOCT_DEDUP), after the steal words
-    [[maybe_unused]] sv4f* dds = reinterpret_cast<sv4f*>(steal) + kStealBytes / 16u + (uint32_t)(tid >> 6) * (kDedupWaveBytes / 16u);
-    const SceneView sc = stage_scene<kLdsScene, kGlobalOct>(a);
+    // the LDS walk on byte-address walk words (stage_scene_walk); kEndW the END word, rootW(sgn) the
+    // root's word for a ray's octant
+    constexpr bool kWalk = RT_WALK_ADDR && kLdsScene && !kGlobalOct;
+    const SceneView sc = kWalk ? stage_scene_walk(a) : stage_scene<kLdsScene, kGlobalOct>(a);
+    const uint32_t kEndW = kWalk ? kEndWalk : a.nNodes;
+    const uint32_t octStride16 = a.octStride * 16u;
+    auto rootW = [&](uint32_t sgn) -> uint32_t { return kWalk ? __umul24(sgn, octStride16) : 0u; };
     if (kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
 
     const F3 camPos{a.camPos[0], a.camPos[1], a.camPos[2]};
@@ -1194,7 +1183,9 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         // ordinary path and the finish queue).
                         if (bounces > 0u && (fused || a.pfKeyIn)) {
                             uint32_t sk;
-                            if (oct_step<kBofs>(sc, a, 0u, cr, kMaxDist, sk) == a.nNodes) {
+                            const uint32_t w0 = kWalk ? oct_step_w<kBofs>(a, rootW(cr.sgn), cr, kMaxDist, sk)
+                                                      : oct_step<kBofs>(sc, a, 0u, cr, kMaxDist, sk);
+                            if (w0 == kEndW) {
                                 bool chain = fused || a.frameCount == 0u;
                                 if (!chain) {
                                     const float4 o = a.result[(uint32_t)g64];
@@ -1258,7 +1249,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                     if (bounces > 0u) {
                         state = kTrav;
                         h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                        cur = 0;
+                        cur = rootW(ray.sgn);
                         if (kStats) ++st.rays;
                     } else {
                         state = kDone;  // no bounce: radiance max(0, 0) = 0
@@ -1332,7 +1323,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if (bounces > 0u) {
                             state = kTrav;
                             h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                            cur = 0;
+                            cur = rootW(ray.sgn);
                             if (kStats) ++st.rays;
                         } else {
                             state = kDone;  // no bounce: radiance max(0, 0) = 0
@@ -1370,7 +1361,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (kLdsScene) {
                 // a walk parked on the END sentinel has finished the reference's traversal
                 // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
-                if (cur == a.nNodes) {
+                if (!kWalk && cur == kEndW) {
                     state = kShade;
                     cur = kNotWalking;
                 }
@@ -1381,11 +1372,12 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 n_leaf = popc_ballot(state == kLeaf);
             }
             if (n_trav + n_leaf == 0u) break;
-            if (popc_ballot(state == kShade) >= kShadeMin) break;
+            // (the byte-address walk: a walk at END is ready to shade; its state is set at shading)
+            if (popc_ballot(kWalk ? cur == kEndWalk : state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
             if (kStats) {
-                u_shadew += popc_ballot(state == kShade);
+                u_shadew += popc_ballot(kWalk ? cur == kEndWalk : state == kShade);
                 u_freew += popc_ballot(state == kIdle || state == kDone);
                 u_other += leaf_step ? n_trav : n_leaf;
                 if (leaf_step) {
@@ -1409,11 +1401,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #if RT_LDS_CONFLICTS
                         if (kStats && !kGlobalOct) {
                             const bool act = cur < kLeafMin;
-                            const uint32_t i = __umul24(ray.sgn, a.octStride) + cur;
+                            const uint32_t i = kWalk ? cur >> 4 : __umul24(ray.sgn, a.octStride) + cur;
                             lds_model(act, i, i & 15u, true, lm[0], lm[1]);
                             const uint32_t strides[2] = {43u, 48u};
                             for (int v = 0; v < 2; ++v) {
-                                const uint32_t iv = ray.sgn * strides[v] + cur;
+                                const uint32_t iv = ray.sgn * strides[v] + (kWalk ? (cur >> 4) - ray.sgn * a.octStride : cur);
                                 lds_model(act, iv, iv & 15u, true, lm[2 + 2 * v], lm[3 + 2 * v]);
                             }
                         }
@@ -1439,20 +1431,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         }
 #endif
                         if (cur < kLeafMin) {
-                            if (kStats && cur != a.nNodes) ++st.visits;
-                            if constexpr (kGlobalOct && kDedupSlots > 0)
-                                cur = oct_step_gd<kBofs>(sc, a, cur, ray, h.t, leaf_i, dds);
-                            else
-                                cur = kGlobalOct ? oct_step_g<kBofs>(sc, a, cur, ray, h.t, leaf_i)
-                                                 : oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
+                            if (kStats && cur != kEndW) ++st.visits;
+                            cur = kGlobalOct ? oct_step_g<kBofs>(sc, a, cur, ray, h.t, leaf_i)
+                                  : kWalk    ? oct_step_w<kBofs>(a, cur, ray, h.t, leaf_i)
+                                             : oct_step<kBofs>(sc, a, cur, ray, h.t, leaf_i);
                         }
-#if RT_BURST_ADAPT
-                        // (diagnostic variant) end the burst early once fewer than
-                        // RT_BURST_ADAPT / 16 of the decision's walking lanes still walk
-                        if (!kGlobalOct && rep >= 2 && rep + 1 < kNodeBurst &&
-                            popc_ballot(cur < a.nNodes) * 16u < n_trav * (uint32_t)RT_BURST_ADAPT)
-                            break;
-#endif
                     } else if (state == kTrav) {
                         if (kStats) ++st.visits;
                         uint32_t next, first = 0, count = 0;
@@ -1474,7 +1457,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
 #if RT_LDS_CONFLICTS
                         if (kStats && !kGlobalOct) {
                             const bool act = (int32_t)cur >= (int32_t)kLeafMin;
-                            const uint32_t t4 = a.octRecords + 3u * (cur & 0x00ffffffu);  // float4 index
+                            const uint32_t t4 = kWalk ? (cur & 0x00ffffffu) >> 4 : a.octRecords + 3u * (cur & 0x00ffffffu);  // float4 index
                             lds_model(act, t4, t4 & 15u, true, lm[6], lm[7]);
                             lds_model(act, t4, (4u * (t4 + 2u)) & 31u, false, lm[8], lm[9]);
                             const uint32_t z = 4u * (a.octRecords + 6u * a.nTris + 4u * a.nMats) + (cur & 0x00ffffffu);
@@ -1499,13 +1482,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                         if ((int32_t)cur >= (int32_t)kLeafMin) {
                             if (kStats) ++st.tests;
                             const uint32_t idx = cur & 0x00ffffffu;
-                            if constexpr (kGlobalOct && kDedupSlots > 0)
-                                tri_accept(tri_eval_gd<M>(sc.tris, idx, ray, dds), (int32_t)idx, h);
-                            else if (kGlobalOct)
+                            if (kGlobalOct)
                                 tri_accept(tri_eval_g<M>(sc.tris, idx, ray), (int32_t)idx, h);
+                            else if (kWalk)  // idx: the record's byte address (h.prim too, until shading)
+                                tri_accept(tri_eval_v<M>(lds_v4_at(idx), lds_v4_at(idx + 16u), lds_f32_at(idx + 32u), ray), (int32_t)idx, h);
                             else
                                 ray_triangle<M>(sc.tris + 3 * idx, (int32_t)idx, ray, h);
-                            cur += 1u - kLeafMin;
+                            cur += (kWalk ? 48u : 1u) - kLeafMin;
                             if (cur < kLeafMin) cur = leaf_i;
                         }
                     } else if (state == kLeaf) {
@@ -1523,13 +1506,15 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
         if (kStats) {
             cyc_trav += tC - tB;
-            const uint32_t ns = popc_ballot(state == kShade);
+            const uint32_t ns = popc_ballot(kWalk ? cur == kEndWalk : state == kShade);
             if (ns) {
                 ++u_srounds;
                 u_slanes += ns;
             }
         }
-        if (state == kShade) {
+        if (kWalk ? cur == kEndWalk : state == kShade) {
+            if (kWalk && h.prim >= 0)  // the walk's byte address -> the triangle index, (addr - base) / 48
+                h.prim = (int32_t)(__umulhi((uint32_t)h.prim - a.octRecords * 16u, 0xAAAAAAABu) >> 5);
             if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension); fused: last frame's
                 const uint32_t last = (a.nFrames - 1u) * a.radStride;
                 if (!fused || gid >= last) {
@@ -1546,7 +1531,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             } else {
                 state = kTrav;
                 h = Traversal{kMaxDist, -1, 0.0f, 0.0f};
-                cur = 0;
+                cur = rootW(ray.sgn);
                 if (kStats) ++st.rays;
             }
         }

@@ -68,15 +68,51 @@ struct MathPinned {
     __device__ __forceinline__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
     __device__ __forceinline__ static float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 #else
-    __device__ __forceinline__ static float rcp(float x) { return 1.0f / x; }
+    // 1.0f / x, correctly rounded, as the hardware reciprocal plus one Newton step (two fma): for
+    // every float with an exponent field in [2, 251] this IS the IEEE quotient, bit for bit
+    // (scripts/probes/pinned_fast_probe.hip, exhaustive: profiles/r06/pinned_fast_probe_v1.txt) --
+    // 6 VALU against the 11 of the IEEE division sequence.  Other operands (0, denormals, |x| >=
+    // 2^125, inf, NaN) take the IEEE division; the branch is wave-uniform.
+    __device__ __forceinline__ static float rcp_fast(float x) {
+        const float y = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
+    }
+    __device__ __forceinline__ static float rcp(float x) {
+        const float r = rcp_fast(x);
+        const bool ok = (__float_as_uint(x) & 0x7fffffffu) - 0x01000000u < 0x7d000000u;
+        if (__builtin_expect(__ballot(!ok) != 0ull, 0)) return ok ? r : 1.0f / x;
+        return r;
+    }
     __device__ __forceinline__ static float div(float a, float b) { return a / b; }
 #endif
 #if RT_PINNED_DIAG_SQRT
     __device__ __forceinline__ static float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
     __device__ __forceinline__ static float rsqrt(float d) { return __builtin_amdgcn_rsqf(d); }
 #else
-    __device__ __forceinline__ static float sqrt(float x) { return __builtin_sqrtf(x); }
-    __device__ __forceinline__ static float rsqrt(float d) { return pm_rsqrt(d); }
+    // sqrt(x), correctly rounded, as the hardware reciprocal square root plus one Markstein step
+    // (s = x*r, h = r/2, s + (x - s*s)*h with fma): for every float with an exponent field in
+    // [25, 254] this IS the IEEE square root, bit for bit (scripts/probes/pinned_fast_probe2.hip,
+    // exhaustive: profiles/r06/pinned_fast_probe_v2.txt) -- 5 VALU against the 14 of the IEEE
+    // sequence.  Other operands (x < 2^-102, negative, 0, inf, NaN) take the IEEE square root.
+    __device__ __forceinline__ static float sqrt_fast(float x) {
+        const float r = __builtin_amdgcn_rsqf(x);
+        const float s = x * r, h = 0.5f * r;
+        return __builtin_fmaf(__builtin_fmaf(-s, s, x), h, s);
+    }
+    __device__ __forceinline__ static float sqrt(float x) {
+        const float f = sqrt_fast(x);
+        const bool ok = __float_as_uint(x) - 0x0c800000u < 0x73000000u;  // exponent field in [25, 254]
+        if (__builtin_expect(__ballot(!ok) != 0ull, 0)) return ok ? f : __builtin_sqrtf(x);
+        return f;
+    }
+    // normalize's 1/sqrt(d): two correctly rounded operations (rt_pinned_math.h pm_rsqrt), here the
+    // two exact sequences above; d >= 2^-126 and finite there (normalize rescales other d first)
+    __device__ __forceinline__ static float rsqrt(float d) {
+        const float f = rcp_fast(sqrt_fast(d));  // (sqrt_fast(d) in [2^-51, 2^64]: rcp_fast's range)
+        const bool ok = __float_as_uint(d) - 0x0c800000u < 0x73000000u;
+        if (__builtin_expect(__ballot(!ok) != 0ull, 0)) return ok ? f : pm_rsqrt(d);
+        return f;
+    }
 #endif
     __device__ __forceinline__ static float dot(F3 a, F3 b) {
         return (a.x * b.x + a.y * b.y) + a.z * b.z;

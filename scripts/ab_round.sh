@@ -14,7 +14,7 @@ for rep in $(seq $reps); do
     if [ $l = main ]; then unset RT_HIP_LIB; else export RT_HIP_LIB=$V/librt_hip_$l.so; fi
     for cfg in "cornell fused" "bunny fused" "cornell per-frame"; do
       set -- $cfg
-      timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 --scene $1 --launch $2 > gpurun_out/ab_last.json 2>&1 || exit 1
+      timeout -k 10 120 python bench.py --no-cpu-baseline --no-configs --steps 10 --scene $1 --launch $2 > gpurun_out/ab_last.json 2>&1 || exit 1
       python3 -c "
 import json
 d = json.loads([l for l in open('gpurun_out/ab_last.json') if l.startswith('{')][-1])

@@ -15,7 +15,7 @@ out=gpurun_out/sweep_$name.txt
 for rep in $(seq $reps); do
   for set in "${sets[@]}"; do
     args=""; for x in $set; do args="$args --tune $x"; done
-    timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 $args "$@" > gpurun_out/sweep_last.json 2>&1 || exit 1
+    timeout -k 10 120 python bench.py --no-cpu-baseline --no-drop-in --no-configs --steps 10 $args "$@" > gpurun_out/sweep_last.json 2>&1 || exit 1
     python3 - "$set" <<'PY' | tee -a $out
 import json, sys
 d = json.loads([l for l in open('gpurun_out/sweep_last.json') if l.startswith('{')][-1])
