@@ -279,8 +279,9 @@ RT_PM_FN int pm_is_odd_int(float y) {
     return ((int32_t)a & 1) != 0;
 }
 
-/* OpenCL/C99 pow special cases, then 2^(y*log2|x|) in fp64, rounded once */
-RT_PM_HEAVY float pm_pow(float x, float y) {
+/* OpenCL/C99 pow special cases, then 2^(y*log2|x|) in fp64, rounded once.  pm_pow_body is the
+ * definition; pm_pow the out-of-line copy most call sites use (same operations, same bits). */
+RT_PM_FN float pm_pow_body(float x, float y) {
     const float qnan = pm_u2f(0x7fc00000u);
     if (y == 0.0f) return 1.0f;
     if (x == 1.0f) return 1.0f;
@@ -310,6 +311,7 @@ RT_PM_HEAVY float pm_pow(float x, float y) {
     else r = (float)pm_exp2_d(z);
     return (neg && yodd) ? -r : r;
 }
+RT_PM_HEAVY float pm_pow(float x, float y) { return pm_pow_body(x, y); }
 
 #ifdef __cplusplus
 }

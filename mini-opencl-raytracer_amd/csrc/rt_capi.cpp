@@ -347,7 +347,8 @@ bool build_oct_nodes(const rt_cl_bvh_node* nd, uint32_t n, const std::vector<uin
 // octants at the same node -- every traversal starts at the root -- read one line, not eight) and
 // larger G keeps neighbouring nodes of one octant together as the octant-major layout does.  Links
 // are stored as walk words (block * 8G + node in block), so the kernel's index (octant x octStride
-// + word) holds with octStride = G; END = the sentinel's word.
+// + word) holds with octStride = G; END = rtk::kEndWalk, a word that is neither a node nor a leaf (a
+// walk that reaches it leaves the node and triangle steps at once: no sentinel loads).
 inline uint32_t goct_word(uint32_t i, uint32_t G) { return (i / G) * 8u * G + i % G; }
 void build_oct_nodes_grouped(const std::vector<uint32_t>& oct, uint32_t n, uint32_t G, std::vector<uint32_t>& out,
                              uint32_t* b_ofs) {
@@ -366,7 +367,7 @@ void build_oct_nodes_grouped(const std::vector<uint32_t>& oct, uint32_t n, uint3
             wb[0] = rb[0];
             wb[1] = rb[1];
             wb[2] = rb[2] >= kLeafMin ? rb[2] : goct_word(rb[2], G);  // leaf code as it is, else the near child
-            wb[3] = goct_word(rb[3], G);
+            wb[3] = rb[3] >= n && RT_GOCT_END_WORD ? rtk::kEndWalk : goct_word(rb[3], G);  // END: the non-walk word
         }
 }
 
@@ -1091,7 +1092,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         a.octStride = RT_GOCT_GROUP;
         a.octB = k->goct_b;
         a.octRecords = 2u * a.octB;
-        a.nNodes = goct_word(k->n_nodes, RT_GOCT_GROUP);  // the END word
+        a.nNodes = RT_GOCT_END_WORD ? rtk::kEndWalk : goct_word(k->n_nodes, RT_GOCT_GROUP);  // the END word
     }
     // (octant walk: refill at 32 free lanes under the pixel-major order, 16 before: -0.5 %,
     // profiles/r05/goct_bursts_weights.txt)

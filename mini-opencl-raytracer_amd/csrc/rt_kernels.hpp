@@ -78,6 +78,12 @@ constexpr uint32_t kRingWaveBytesPf = kRingSlots * 16u + kRingSlots * 4u;  // pe
 // step schedule: per workgroup, each wave's remaining chunk {next, end} (64-bit word per wave),
 // from which its siblings take single tiles once the work counter is dry
 constexpr uint32_t kStealBytes = 4u * 8u + 32u;  // (padded to whole float4s)
+// END as a walk word that is neither a node (< 2^24) nor a leaf code (count << 24 | first, count
+// 1..127): the step schedule's byte-address LDS walk and its octant walk over HBM/L2 (step_body)
+constexpr uint32_t kEndWalk = 0xff000000u;
+#ifndef RT_GOCT_END_WORD
+#define RT_GOCT_END_WORD 1  // the HBM/L2 octant walk's END as kEndWalk (0: its sentinel's word, visited)
+#endif
 
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address

@@ -170,7 +170,6 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a) {
 #ifndef RT_WALK_ADDR
 #define RT_WALK_ADDR 1
 #endif
-constexpr uint32_t kEndWalk = 0xff000000u;  // END as a byte-address walk word: neither a node nor a leaf
 __device__ __forceinline__ uint32_t walk_word(uint32_t w, uint32_t octant, const KernelArgs& a) {
     if (w >= kLeafMin) return (w & 0xff000000u) | (a.octRecords * 16u + (w & 0x00ffffffu) * 48u);
     if (w >= a.nNodes) return kEndWalk;
@@ -520,7 +519,7 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     if (spec) {
         (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
         const float r = next_rand(seed);
-        c = M::pow(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
+        c = M::pow_shade(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
         sinT = M::sqrt(M::max(0.0f, madd<M>(-c, c, 1.0f)));
     } else {
         const float s2 = next_rand(seed);
@@ -994,7 +993,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // root's word for a ray's octant
     constexpr bool kWalk = RT_WALK_ADDR && kLdsScene && !kGlobalOct;
     const SceneView sc = kWalk ? stage_scene_walk(a) : stage_scene<kLdsScene, kGlobalOct>(a);
-    const uint32_t kEndW = kWalk ? kEndWalk : a.nNodes;
+    // END as a word that is neither a node nor a leaf (kEndWalk): the byte-address LDS walk and the octant
+    // walk over HBM/L2 (whose END links the host writes so, a.nNodes = kEndWalk): a walk at END is
+    // ready to shade, with no sentinel visits (no sentinel loads on the HBM/L2 walk) and no END test
+    constexpr bool kEndWord = kWalk || (kGlobalOct && RT_GOCT_END_WORD);
+    const uint32_t kEndW = kEndWord ? kEndWalk : a.nNodes;
     const uint32_t octStride16 = a.octStride * 16u;
     auto rootW = [&](uint32_t sgn) -> uint32_t { return kWalk ? __umul24(sgn, octStride16) : 0u; };
     if (kGlobalOct) __syncthreads();  // (stage_scene stages nothing for this walk)
@@ -1361,7 +1364,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             if (kLdsScene) {
                 // a walk parked on the END sentinel has finished the reference's traversal
                 // (kernel_bvh.cl:181-218, stack empty): it is ready to shade
-                if (!kWalk && cur == kEndW) {
+                if (!kEndWord && cur == kEndW) {
                     state = kShade;
                     cur = kNotWalking;
                 }
@@ -1373,11 +1376,11 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             }
             if (n_trav + n_leaf == 0u) break;
             // (the byte-address walk: a walk at END is ready to shade; its state is set at shading)
-            if (popc_ballot(kWalk ? cur == kEndWalk : state == kShade) >= kShadeMin) break;
+            if (popc_ballot(kEndWord ? cur == kEndWalk : state == kShade) >= kShadeMin) break;
             if (!exhausted && popc_ballot(state == kIdle || state == kDone) >= kRefillMin) break;
             const bool leaf_step = n_leaf * a.stepWeightNode > n_trav * a.stepWeightLeaf;
             if (kStats) {
-                u_shadew += popc_ballot(kWalk ? cur == kEndWalk : state == kShade);
+                u_shadew += popc_ballot(kEndWord ? cur == kEndWalk : state == kShade);
                 u_freew += popc_ballot(state == kIdle || state == kDone);
                 u_other += leaf_step ? n_trav : n_leaf;
                 if (leaf_step) {
@@ -1506,13 +1509,13 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         uint64_t tC = kStats ? __builtin_amdgcn_s_memtime() : 0;
         if (kStats) {
             cyc_trav += tC - tB;
-            const uint32_t ns = popc_ballot(kWalk ? cur == kEndWalk : state == kShade);
+            const uint32_t ns = popc_ballot(kEndWord ? cur == kEndWalk : state == kShade);
             if (ns) {
                 ++u_srounds;
                 u_slanes += ns;
             }
         }
-        if (kWalk ? cur == kEndWalk : state == kShade) {
+        if (kEndWord ? cur == kEndWalk : state == kShade) {
             if (kWalk && h.prim >= 0)  // the walk's byte address -> the triangle index, (addr - base) / 48
                 h.prim = (int32_t)(__umulhi((uint32_t)h.prim - a.octRecords * 16u, 0xAAAAAAABu) >> 5);
             if (bounce == 0u && a.hitIds) {  // primary hit outputs (extension); fused: last frame's

@@ -28,7 +28,7 @@ for step in "$@"; do
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu --maxfail 8 -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-configs ;;
     dist1) run dist1_rccl 300 python bench.py --force-dist --check-gather --steps 5 --warmup 1 --no-cpu-baseline && \
            run dist1_rccl_sync 300 python bench.py --force-dist --gather-sync --steps 5 --warmup 1 --no-cpu-baseline ;;
     pmc) run pmc_default 900 bash scripts/profile.sh default ;;
@@ -43,18 +43,21 @@ for step in "$@"; do
                  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     #   final_bench: PMC records (headline + bunny -> profiles/pmc.json), the default bench with its CPU
     #   baseline and drop-in figures, and a kernel trace of the timed loop
+    #   (round 6: also the PMC keys of the bench line's other configs -- bench.py EXTRA_CONFIGS)
     final_bench) run pmc_default 900 bash scripts/profile.sh default && \
                  run pmc_bunny 900 bash scripts/profile.sh bunny --scene bunny && \
-                 cp gpurun_out/pmc_bunny/pmc.json profiles/pmc.json && \
+                 run pmc_1080p 900 bash scripts/profile.sh 1080p --width 1920 --height 1080 --bounces 2 --frames 1 && \
+                 run pmc_pinned 900 bash scripts/profile.sh pinned --math pinned && \
+                 cp gpurun_out/pmc_pinned/pmc.json profiles/pmc.json && \
                  run bench_default 600 python bench.py && \
-                 run bench_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/final_trace -o run -- python bench.py --steps 20 --warmup 1 --no-cpu-baseline --no-drop-in ;;
+                 run bench_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/final_trace -o run -- python bench.py --steps 20 --warmup 1 --no-cpu-baseline --no-drop-in --no-configs ;;
     #   final_configs: the other configs (no CPU baseline / drop-in) and the emulated ranks
     final_configs) for c in "bunny --scene bunny" "perframe --launch per-frame --steps 5" "pinned --math pinned --steps 5" \
                              "1080p --width 1920 --height 1080 --bounces 2 --frames 1 --steps 20" \
                              "512 --width 512 --height 512 --bounces 1 --frames 1 --steps 50" \
                              "bunny_perframe --scene bunny --launch per-frame --steps 3"; do
                      set -- $c; n=$1; shift
-                     run bench_$n 300 python bench.py --no-cpu-baseline --no-drop-in "$@"
+                     run bench_$n 300 python bench.py --no-cpu-baseline --no-drop-in --no-configs "$@"
                    done
                    for sc in cornell bunny; do
                      RT_EMU_SCENE=$sc run rank_emulation_$sc 600 python scripts/rank_emulation.py
