@@ -374,6 +374,8 @@ def roofline(args, world, frames_per_launch, kernel_ms, period_ms, local_counts,
           "kernel_ms": round(kernel_ms, 4), "period_ms": round(period_ms, 4) if period_ms > 0 else None,
           "frames_per_launch": frames_per_launch, "lane_util": None, "hbm_frac": None,
           "alg_bytes_per_launch": int(alg_bytes),
+          "alg_note": "SURVEY 8(d) byte model (48 B per node visit and triangle test, 164 B per closest hit, "
+                      "32 B per pixel): mostly LDS reads, not HBM traffic -- not a bound; HBM is `traffic`",
           "alg_gbs": round(alg_bytes / (launch_ms * 1e-3) / 1e9, 2) if launch_ms > 0 else None,
           "pmc": None}
     kernel_ms = launch_ms

@@ -519,7 +519,7 @@ __device__ __forceinline__ F3 sample_brdf(F3 wo, F3& wi, float& pdf, F3 n, const
     if (spec) {
         (void)next_rand(seed);  // `xi`, drawn and unused (kernel_bvh.cl:230)
         const float r = next_rand(seed);
-        c = M::pow_shade(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
+        c = M::pow(r, m.inv_a1);  // cosTheta = pow(r, 1 / (alpha + 1))
         sinT = M::sqrt(M::max(0.0f, madd<M>(-c, c, 1.0f)));
     } else {
         const float s2 = next_rand(seed);

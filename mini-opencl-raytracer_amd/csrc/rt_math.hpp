@@ -60,9 +60,6 @@ __device__ __forceinline__ F3 operator-(F3 a) { return F3{-a.x, -a.y, -a.z}; }
 #ifndef RT_PINNED_DIAG_TRIG
 #define RT_PINNED_DIAG_TRIG 0
 #endif
-#ifndef RT_PINNED_POW_INLINE
-#define RT_PINNED_POW_INLINE 0
-#endif
 struct MathPinned {
     static constexpr int kId = 0;
     static constexpr bool kContract = false;
@@ -125,16 +122,9 @@ struct MathPinned {
     }
 #if RT_PINNED_DIAG_POW
     __device__ __forceinline__ static float pow(float x, float y) { return ::powf(x, y); }
-    __device__ __forceinline__ static float pow_shade(float x, float y) { return ::powf(x, y); }
 #else
+    // (out of line; inlining the BRDF's call into the render costs 13 %: profiles/r06/pinned_ab.txt)
     __device__ __forceinline__ static float pow(float x, float y) { return pm_pow(x, y); }
-    // the BRDF's one pow per specular sample (kernel_bvh.cl:231): the same definition inlined into
-    // the render (RT_PINNED_POW_INLINE) or called out of line like the accumulation's six
-#if RT_PINNED_POW_INLINE
-    __device__ __forceinline__ static float pow_shade(float x, float y) { return pm_pow_body(x, y); }
-#else
-    __device__ __forceinline__ static float pow_shade(float x, float y) { return pm_pow(x, y); }
-#endif
 #endif
     // pow(x, 2.0f) call sites of the reference (kernel_bvh.cl:224, :275): pinned as the
     // exact square, as LLVM's libcall simplifiers fold it (rt_pinned_math.h)
@@ -171,7 +161,6 @@ struct MathDeviceLib {
     }
     __device__ __forceinline__ static float rsqrt(float d) { return ::rsqrtf(d); }
     __device__ __forceinline__ static float pow(float x, float y) { return ::powf(x, y); }
-    __device__ __forceinline__ static float pow_shade(float x, float y) { return ::powf(x, y); }
     // the AMD OpenCL compiler folds pow(x, 2.0f) to x*x (AMDGPU libcall simplification;
     // visible in the reference's IR: DistributionGGX, SampleSpecular)
     __device__ __forceinline__ static float pow2(float x) { return x * x; }
