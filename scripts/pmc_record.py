@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -21,9 +22,13 @@ sys.path.insert(0, REPO)
 
 
 def render_kernel(names):
-    """The timed render launch: KernelEntry's step entry point without the stats variant (its
-    first template argument, kStats, false)."""
-    c = [k for k in names if "kernel_entry" in k and "<false" in k]
+    """The timed render launch: KernelEntry's step entry point specialised for a launch kind (its
+    last template argument, kMode, 1 fused or 2 per-frame; the stats variant that the count pass
+    runs is the generic body, kMode 0), else -- other schedules -- the entry point whose first
+    template argument, kStats, is false."""
+    c = [k for k in names if "kernel_entry" in k and re.search(r", [12]>", k)]
+    if not c:
+        c = [k for k in names if "kernel_entry" in k and "<false" in k]
     return c[0] if c else None
 
 

@@ -32,3 +32,20 @@ def test_default_bench_line_carries_every_config():
     # flip a hit (SURVEY.md 7 hard part 1), by far less than a percent
     rel = abs(cfg["cfg3_pinned"]["rays_per_step"] - line["config"]["rays_per_step"]) / line["config"]["rays_per_step"]
     assert rel < 1e-3
+
+
+def test_every_bench_config_has_a_pmc_record():
+    """CPU: the headline and every extra config of the default bench line are priced by a
+    profiles/pmc.json record (scripts/profile.sh); `stale` in the line says whether the record was
+    measured on the current kernel sources."""
+    import bench
+    db = json.load(open(os.path.join(REPO, "profiles", "pmc.json")))
+    base = bench.parse([])
+    keys = [bench.workload_key(base, 1, base.frames)]
+    for _, over, _, _ in bench.EXTRA_CONFIGS:
+        a = bench.parse([])
+        a.__dict__.update(over)
+        keys.append(bench.workload_key(a, 1, a.frames if a.frames > 1 else 1))
+    missing = [k for k in keys if k not in db]
+    assert not missing, f"no PMC record for {missing} (run scripts/profile.sh)"
+    assert len(set(keys)) == len(keys)
