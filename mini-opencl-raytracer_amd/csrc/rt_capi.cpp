@@ -37,6 +37,19 @@ constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene pa
 #ifndef RT_TIMELINE
 #define RT_TIMELINE 0
 #endif
+#ifndef RT_STATIC_FIRST
+#define RT_STATIC_FIRST 1
+#endif
+#ifndef RT_PF_COUNTER_SLOTS
+#define RT_PF_COUNTER_SLOTS 1
+#endif
+// tail chunks: sized so that every `RT_TAIL_SHARE_WAVES` waves get >= 2.5 of them (1: every wave; 4:
+// every workgroup, whose waves split the last one by work stealing): fewer atomics on the tail
+// counter for small launches (1080p 2-bounce frames 0.282 -> 0.218 ms alone; 4K launches already
+// take the largest chunk, profiles/r06/work_handout_ab.txt)
+#ifndef RT_TAIL_SHARE_WAVES
+#define RT_TAIL_SHARE_WAVES 4
+#endif
 // diagnostic timeline builds (-DRT_TIMELINE=1, scripts/timeline.py) write three 64-bin histograms after
 // the primary hit ids: such a build requires hit buffers that long
 constexpr size_t kHitPad = RT_TIMELINE ? 192 : 0;
@@ -73,6 +86,7 @@ struct rt_kernel_s {
     uint32_t* work_counter = nullptr;  // persistent schedules' chunk counters: [4] per render stream
     uint32_t* accum_key = nullptr;     // sky-shortcut keys: [0..3] fused frames, [4..5] per-frame (zeroed once)
     int pf_parity = 0;                 // per-frame key slot read by the next launch
+    int pf_ctr = 0;                    // per-frame chunk-counter slot of the next launch (RT_PF_COUNTER_SLOTS)
     int tile_major = -1;               // fused work order: -1 auto, 0 frame-major, 1 tile-major, 2 pixel-major
     int pf_sky = 1;                    // per-frame sky shortcut: 0 off, 1 large launches, 2 always
     int pf_defer = 2;                  // per-frame step launches through radiance slots + accumulation
@@ -715,8 +729,8 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * (RT_RAD_SETS + 1));
-    if (e == hipSuccess) e = hipMemsetAsync(k->work_counter, 0, 16 * (RT_RAD_SETS + 1), qs(ctx));
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * (RT_RAD_SETS + 2));
+    if (e == hipSuccess) e = hipMemsetAsync(k->work_counter, 0, 16 * (RT_RAD_SETS + 2), qs(ctx));
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
     if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
@@ -1007,7 +1021,9 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     const uint64_t n_tiles = tilesY * a.tilesX;
     if (n_tiles * 64 > 0xfff00000ull) return RT_INVALID_GLOBAL_WORK_SIZE;
     a.nTiles = (uint32_t)n_tiles;
-    a.workCounter = k->work_counter + 4 * RT_RAD_SETS;  // per-frame launches: their own counters
+    // per-frame launches: their own counters (two slots in turn with RT_PF_COUNTER_SLOTS, below)
+    a.workCounter = k->work_counter + 4 * RT_RAD_SETS;
+    a.workCounterClear = nullptr;
     a.chunkPixels = k->chunk_pixels ? k->chunk_pixels : 512u;  // (the launch's order decides below)
     a.tailChunk = k->tail_chunk;
     a.refillMin = k->refill_min;
@@ -1173,10 +1189,19 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // gives every wave >= 2.5 of them -- few atomics on the tail counter for large launches,
         // fine-grained balance for small ones (4K fused 256, 4K per-frame / 1080p / 512^2 fused 128,
         // 512^2 per-frame 64: profiles/r02/chunk_sweep.txt)
-        const uint64_t share = (tot - a.chunkSplit) / waves;
+        const uint64_t share = (tot - a.chunkSplit) * RT_TAIL_SHARE_WAVES / waves;
         uint32_t tail = 64;
         while (tail * 2u <= k->tail_chunk && (uint64_t)tail * 2u * 5u <= share * 2u) tail *= 2u;
         a.tailChunk = tail;
+        // RT_STATIC_FIRST: a per-frame launch without a bulk region starts every wave on its own tail chunk,
+        // with no atomic (step_body), and the tail counter hands out from past those chunks.  (The
+        // same for the bulk region of large launches was 3-5 % slower: the waves then stay in step
+        // and meet again at the counter.)
+        a.tailBase = a.chunkSplit;
+        if (RT_STATIC_FIRST && !fused && si == RT_SCHED_STEP && !wf && a.chunkSplit == 0u) {
+            a.staticFirst = 1u;
+            a.tailBase = (uint32_t)std::min<uint64_t>(waves * tail, tot);
+        }
     }
 
     // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch
@@ -1244,7 +1269,14 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
 #else
     const bool clear_here = !fused;
 #endif
-    if (si != RT_SCHED_TILES && !wf && clear_here) {
+    // RT_PF_COUNTER_SLOTS: a per-frame step launch takes one of two counter slots in turn and zeroes
+    // the other for the next one (step_body), so no clearing launch sits between consecutive renders
+    // (1080p: a 4-us fill and two ~6-us dispatch gaps in a ~0.28-ms frame)
+    const bool pf_slots = RT_PF_COUNTER_SLOTS && !fused && si == RT_SCHED_STEP && !wf;
+    if (pf_slots) {
+        a.workCounter = k->work_counter + 4 * (RT_RAD_SETS + k->pf_ctr);
+        a.workCounterClear = k->work_counter + 4 * (RT_RAD_SETS + (k->pf_ctr ^ 1));
+    } else if (si != RT_SCHED_TILES && !wf && clear_here) {
         hipError_t me = hipMemsetAsync(a.workCounter, 0, 16, rstr);
         if (me != hipSuccess) return map_hip(me);
     }
@@ -1264,6 +1296,7 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         k->pending_events.emplace_back(ev0, ev1);
     }
     if (a.pfKeyIn) k->pf_parity ^= 1;
+    if (pf_slots) k->pf_ctr ^= 1;
     if (fused) {
         // fused frames: the gamma accumulation of every frame, in order, per pixel -- on the
         // accumulation stream after this render, overlapping whatever the main stream runs next

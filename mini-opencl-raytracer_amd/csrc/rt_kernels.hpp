@@ -58,6 +58,10 @@ struct KernelArgs {
     // pfKeyIn = the value all-sky pixels hold if they followed the chain, pfKeyOut = this launch's
     const uint32_t* pfKeyIn;
     uint32_t* pfKeyOut;
+    // (appended fields: the earlier ones keep their offsets)
+    uint32_t* workCounterClear;         // per-frame step launches: the other counter slot, zeroed by this launch
+    uint32_t tailBase;                  // first tail work item the tail counter hands out (next_chunk)
+    uint32_t staticFirst;               // step schedule: waves start with their own tail chunk (no bulk region)
 };
 
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place

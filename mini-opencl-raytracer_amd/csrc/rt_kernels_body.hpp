@@ -770,6 +770,10 @@ __device__ __forceinline__ float4 rad_load(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Tail chunks come from a.tailBase on: the end of the bulk region, or -- per-frame launches whose
+// first chunks are handed out statically (a.staticFirst, rt_capi.cpp) -- past those chunks
+// (kFusedOnly: bodies for fused launches only, which never start statically: the bulk region's end).
+template <bool kFusedOnly>
 __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
                                            uint32_t& len, bool& tail) {
     uint32_t b = 0;
@@ -784,7 +788,7 @@ __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, 
         tail = true;  // this wave never asks the bulk counter again
     }
     if (lane == 0) b = atomicAdd(&a.workCounter[1], a.tailChunk);
-    b = __shfl(b, 0, 64) + a.chunkSplit;
+    b = __shfl(b, 0, 64) + (kFusedOnly ? a.chunkSplit : a.tailBase);
     if (b >= total) return false;
     base = b;
     len = min(a.tailChunk, total - b);
@@ -840,6 +844,9 @@ __device__ __forceinline__ void finish_queued(const KernelArgs& a, const float4*
 // lane-wait counters
 #ifndef RT_TIMELINE
 #define RT_TIMELINE 0
+#endif
+#ifndef RT_TIMELINE_DIV
+#define RT_TIMELINE_DIV 1
 #endif
 #ifndef RT_TRI_BURST
 #define RT_TRI_BURST 2
@@ -932,6 +939,7 @@ __device__ __noinline__ void lds_model(bool act, uint32_t key, uint32_t bank, bo
 // hold whole chunks.  64-bit LDS atomics hand out every tile exactly once, whoever takes it, so
 // the results cannot change (seeds follow the work item, kernel_bvh.cl:445).  Emulated N = 8 rank
 // step -4 %, per-frame 4K launches -5 % (profiles/r03/steal_ab.txt).
+template <bool kFusedOnly>
 __device__ __forceinline__ bool take_tile(const KernelArgs& a, unsigned long long* steal, uint32_t me, uint32_t lane,
                                           uint32_t total, uint32_t& chunk_base, uint32_t& chunk_len, bool& chunk_tail,
                                           bool& dry, uint32_t& unit) {
@@ -943,7 +951,7 @@ __device__ __forceinline__ bool take_tile(const KernelArgs& a, unsigned long lon
             unit = (uint32_t)old;
             return true;
         }
-        if (next_chunk(a, total, lane, chunk_base, chunk_len, chunk_tail)) {
+        if (next_chunk<kFusedOnly>(a, total, lane, chunk_base, chunk_len, chunk_tail)) {
             if (lane == 0)
                 (void)atomicExch(&steal[me], ((unsigned long long)(chunk_base + chunk_len) << 32) |
                                                  (unsigned long long)(chunk_base + 64u));
@@ -987,8 +995,27 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
         steal = reinterpret_cast<unsigned long long*>(
             smem_s + lds_scene_f4<kLdsScene, kGlobalOct>(a) + (fused ? 0u : 4u * kFinishSlots) +
             (kRingLds ? 4u * (fused ? kRingWaveBytes / 16u : kRingWaveBytesPf / 16u) : 0u));
-        if (tid < 4) steal[tid] = 0ull;  // published by stage_scene's barrier (or the one below)
+        // published by stage_scene's barrier (or the one below).  a.staticFirst (launches without
+        // a bulk region, rt_capi.cpp): each wave starts with its own tail chunk -- chunk (global wave
+        // index) -- as its range, taken with no atomic: every resident wave asks for work at once
+        // when a launch starts, and one address's returning atomics serialise at the L2
+        // (1080p 2-bounce frames 0.282 -> 0.235 ms alone, profiles/r06/work_handout_ab.txt).  The
+        // tail counter then hands out from past these chunks (a.tailBase): every work item is still
+        // handed out exactly once.
+        if (tid < 4) {
+            unsigned long long r = 0ull;
+            if (!fused && a.staticFirst) {
+                const uint32_t tot = a.nTiles * 64u * (fused ? a.nFrames : 1u);
+                const uint32_t b0 = (blockIdx.x * 4u + (uint32_t)tid) * a.tailChunk;
+                if (b0 < tot) r = ((unsigned long long)min(b0 + a.tailChunk, tot) << 32) | b0;
+            }
+            steal[tid] = r;
+        }
     }
+    // per-frame launches alternate between two counter slots: this launch zeroes the one the next
+    // launch takes (same stream, so that launch sees it) instead of a clearing launch in front of
+    // each render (rt_capi.cpp)
+    if (!fused && a.workCounterClear && blockIdx.x == 0 && tid < 4) a.workCounterClear[tid] = 0u;
     // the LDS walk on byte-address walk words (stage_scene_walk); kEndW the END word, rootW(sgn) the
     // root's word for a ray's octant
     constexpr bool kWalk = RT_WALK_ADDR && kLdsScene && !kGlobalOct;
@@ -1151,7 +1178,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 if (idle == 0ull) break;
                 if (rc_n == 0u) {
                     uint32_t unit = 0;  // the tile's first work item in the work order (wave-uniform)
-                    if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
+                    if (!take_tile<kMode == 1>(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
                                    chunk_tail, dry, unit)) {
                         exhausted = true;
 #if RT_TIMELINE
@@ -1271,7 +1298,7 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
                 if (idle == 0ull) break;
                 // tile_unit: the current tile's first work item, tile_used of its 64 handed out
                 if (tile_used >= 64u) {
-                    if (!take_tile(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
+                    if (!take_tile<kMode == 1>(a, steal, (uint32_t)tid >> 6, (uint32_t)lane, total, chunk_base, chunk_len,
                                    chunk_tail, dry, tile_unit)) {
                         exhausted = true;
                         break;
@@ -1571,12 +1598,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             atomicAdd(&a.stats[18], (unsigned long long)rt_end);
             atomicAdd(&a.stats[19], 1ull);
             if (a.hitIds) {
-                // lifetime (40 us bins), counter-dry time (40 us bins), end - dry (10 us bins)
-                const uint32_t bin = min((uint32_t)((rt_end - rt_start) / 4000ull), 63u);
+                // lifetime (40 us bins), counter-dry time (40 us bins), end - dry (10 us bins); all
+                // RT_TIMELINE_DIV times finer in builds for short launches
+                constexpr uint64_t kBin = 4000ull / RT_TIMELINE_DIV, kBinTail = 1000ull / RT_TIMELINE_DIV;
+                const uint32_t bin = min((uint32_t)((rt_end - rt_start) / kBin), 63u);
                 atomicAdd(&a.hitIds[a.width * a.height + bin], 1);
                 const uint64_t dry_at = rt_dry ? rt_dry : rt_end;
-                atomicAdd(&a.hitIds[a.width * a.height + 64u + min((uint32_t)((dry_at - rt_start) / 4000ull), 63u)], 1);
-                atomicAdd(&a.hitIds[a.width * a.height + 128u + min((uint32_t)((rt_end - dry_at) / 1000ull), 63u)], 1);
+                atomicAdd(&a.hitIds[a.width * a.height + 64u + min((uint32_t)((dry_at - rt_start) / kBin), 63u)], 1);
+                atomicAdd(&a.hitIds[a.width * a.height + 128u + min((uint32_t)((rt_end - dry_at) / kBinTail), 63u)], 1);
             }
 #else
             atomicAdd(&a.stats[15], (unsigned long long)u_rlanes);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase wave-cycle shares of the step schedule (stats variant, s_memtime).
 Usage: phase_profile.py [step]   (env: RT_PHASE_SCENE=bunny, RT_PHASE_MATH, RT_PHASE_LB, RT_PHASE_FRAMES,
-RT_PHASE_TUNE=name=value,...)"""
+RT_PHASE_TUNE=name=value,..., RT_PHASE_W, RT_PHASE_H)"""
 import os
 import sys
 
@@ -25,7 +25,8 @@ for name in scheds:
   lbs = [int(x) for x in os.environ.get("RT_PHASE_LB", "1,9").split(",")]
   for math in maths:
     for lb in lbs:
-        r = HipRenderer(sc, 3840, 2160, math=math, stats=True, sched=sched)
+        r = HipRenderer(sc, int(os.environ.get("RT_PHASE_W", "3840")), int(os.environ.get("RT_PHASE_H", "2160")),
+                        math=math, stats=True, sched=sched)
         for t in filter(None, os.environ.get("RT_PHASE_TUNE", "").split(",")):  # name=value,...
             r.k.set_tuning(t.split("=")[0], int(t.split("=")[1]))
         nf = int(os.environ.get("RT_PHASE_FRAMES", "8"))
