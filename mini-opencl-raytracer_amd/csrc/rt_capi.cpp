@@ -72,6 +72,7 @@ struct rt_kernel_s {
     // -0.3 %, per-frame -0.5 %, profiles/r03/shade_threshold_sweep.txt); scenes read from HBM/L2
     // keep 8 / 48
     uint32_t refill_min = 6, shade_min = 48;
+    bool refill_min_set = false;  // RT_TUNE_REFILL_MIN given: also for small per-frame launches (below)
     // scenes read from HBM/L2: 0 = auto (64-B node records 8 / 48; octant records 16 / 48,
     // profiles/r02/goct_sweep.txt)
     uint32_t refill_min_g = 0, shade_min_g = 0;
@@ -1201,13 +1202,19 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if (RT_STATIC_FIRST && !fused && si == RT_SCHED_STEP && !wf && a.chunkSplit == 0u) {
             a.staticFirst = 1u;
             a.tailBase = (uint32_t)std::min<uint64_t>(waves * tail, tot);
+            // such launches (a 1080p frame: ~400 work items per wave) refill at 16 free lanes, not 6:
+            // 1080p 2-bounce frames -2.8 % (4K fused launches lose 5 % at 16,
+            // profiles/r06/work_handout_ab.txt)
+            if (lds && !k->refill_min_set) a.refillMin = 16u;
         }
     }
 
     // per-frame sky shortcut (step_body): its key costs each wave one gamma step at launch
-    // start, which pays off from ~1k pixels per wave (4K) and not on small frames (512^2, 1080p)
+    // start, which pays off from ~256 pixels per wave (1080p -2.7 %, 4K) and not on small frames
+    // (512^2; round 6: the threshold was 1k pixels per wave before the small-launch hand-out,
+    // profiles/r06/work_handout_ab.txt)
     if (!fused && si == RT_SCHED_STEP &&
-        (k->pf_sky == 2 || (k->pf_sky == 1 && g1 - g0 >= 1024u * 4u * grid))) {
+        (k->pf_sky == 2 || (k->pf_sky == 1 && g1 - g0 >= 256u * 4u * grid))) {
         a.pfKeyIn = k->accum_key + 4 + k->pf_parity;
         a.pfKeyOut = k->accum_key + 4 + (k->pf_parity ^ 1);
     }
@@ -1681,7 +1688,11 @@ int rtKernelSetTuning(rt_kernel k, int param, int value) {
     flush_kernel(k);
     auto in = [&](int lo, int hi) { return value >= lo && value <= hi; };
     switch (param) {
-        case RT_TUNE_REFILL_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->refill_min = (uint32_t)value; break;
+        case RT_TUNE_REFILL_MIN:
+            if (!in(1, 64)) return RT_INVALID_VALUE;
+            k->refill_min = (uint32_t)value;
+            k->refill_min_set = true;
+            break;
         case RT_TUNE_SHADE_MIN: if (!in(1, 64)) return RT_INVALID_VALUE; k->shade_min = (uint32_t)value; break;
         case RT_TUNE_REFILL_MIN_GLOBAL: if (!in(0, 64)) return RT_INVALID_VALUE; k->refill_min_g = (uint32_t)value; break;
         case RT_TUNE_SHADE_MIN_GLOBAL: if (!in(0, 64)) return RT_INVALID_VALUE; k->shade_min_g = (uint32_t)value; break;

@@ -1,0 +1,13 @@
+set -u
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/c2_suite.txt 2>&1 || { tail -30 gpurun_out/c2_suite.txt; exit 1; }
+tail -1 gpurun_out/c2_suite.txt
+for r in 1 2 3; do
+ for cfg in "c2|--width 1920 --height 1080 --bounces 2 --frames 1 --steps 40" "pf4k|--launch per-frame" "c512pf|--width 512 --height 512 --bounces 9 --frames 8 --launch per-frame"; do
+  n=${cfg%%|*}; args=${cfg#*|}
+  timeout -k 10 120 python bench.py --no-cpu-baseline --no-configs --no-drop-in --steps 10 $args > gpurun_out/c2_last.json 2>&1 || exit 1
+  python3 -c "
+import json
+d = json.loads([l for l in open('gpurun_out/c2_last.json') if l.startswith('{')][-1])
+print('$n', 'ms/frame', d['ms_per_frame'], 'launch_ms', d['roofline'].get('launch_ms'))"
+ done
+done
