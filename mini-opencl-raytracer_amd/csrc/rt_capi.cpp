@@ -40,6 +40,12 @@ constexpr size_t kLdsBudget = 64 * 1024;       // per-workgroup LDS the scene pa
 #ifndef RT_STATIC_FIRST
 #define RT_STATIC_FIRST 1
 #endif
+// per-frame launches without a bulk region: tail counters on this many partitions (a power of two, <=
+// rtk::kMaxParts; step_body next_chunk_parts) -- 1080p 2-bounce frames 0.172 -> 0.165 ms with 128-pixel
+// tail chunks, which on one counter took 0.231 (profiles/r06/work_handout_ab.txt)
+#ifndef RT_COUNTER_PARTS
+#define RT_COUNTER_PARTS 8
+#endif
 #ifndef RT_PF_COUNTER_SLOTS
 #define RT_PF_COUNTER_SLOTS 1
 #endif
@@ -730,8 +736,11 @@ int rtCreateKernel(rt_context ctx, const char* name, rt_kernel* out) {
     if (!k) return RT_OUT_OF_HOST_MEMORY;
     k->ctx = ctx;
     hipError_t e = hipMalloc(&k->dstats, kStatWords * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc(&k->work_counter, 16 * (RT_RAD_SETS + 2));
-    if (e == hipSuccess) e = hipMemsetAsync(k->work_counter, 0, 16 * (RT_RAD_SETS + 2), qs(ctx));
+    // fused radiance sets' counters (16 B each), then the two per-frame slots of kMaxParts counter
+    // partitions kPartStride words apart
+    const size_t wc_bytes = 16 * RT_RAD_SETS + 2 * sizeof(uint32_t) * rtk::kMaxParts * rtk::kPartStride;
+    if (e == hipSuccess) e = hipMalloc(&k->work_counter, wc_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(k->work_counter, 0, wc_bytes, qs(ctx));
     if (e == hipSuccess) e = hipMalloc(&k->accum_key, 32);
     if (e == hipSuccess) e = hipMemsetAsync(k->accum_key, 0, 32, qs(ctx));
     if (e == hipSuccess) e = hipMemsetAsync(k->dstats, 0, kStatWords * sizeof(unsigned long long), qs(ctx));
@@ -1190,7 +1199,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         // gives every wave >= 2.5 of them -- few atomics on the tail counter for large launches,
         // fine-grained balance for small ones (4K fused 256, 4K per-frame / 1080p / 512^2 fused 128,
         // 512^2 per-frame 64: profiles/r02/chunk_sweep.txt)
-        const uint64_t share = (tot - a.chunkSplit) * RT_TAIL_SHARE_WAVES / waves;
+        // (with counter partitions -- per-frame launches without a bulk region, below -- the grabs no
+        // longer queue on one address, and the finer per-wave rule balances better)
+        const bool parts = RT_COUNTER_PARTS > 1 && RT_STATIC_FIRST && RT_PF_COUNTER_SLOTS && !fused &&
+                           si == RT_SCHED_STEP && !wf && a.chunkSplit == 0u && grid >= RT_COUNTER_PARTS &&
+                           tot >= 256u * waves;  // (512^2 frames, ~50 work items per wave: +5 % with them)
+        const uint64_t share = (tot - a.chunkSplit) * (parts ? 1u : RT_TAIL_SHARE_WAVES) / waves;
         uint32_t tail = 64;
         while (tail * 2u <= k->tail_chunk && (uint64_t)tail * 2u * 5u <= share * 2u) tail *= 2u;
         a.tailChunk = tail;
@@ -1202,6 +1216,12 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
         if (RT_STATIC_FIRST && !fused && si == RT_SCHED_STEP && !wf && a.chunkSplit == 0u) {
             a.staticFirst = 1u;
             a.tailBase = (uint32_t)std::min<uint64_t>(waves * tail, tot);
+            // RT_COUNTER_PARTS: the tail counter split over that many partitions (with the per-frame
+            // counter slots, whose layout holds them)
+            if (parts) {
+                a.nParts = RT_COUNTER_PARTS;
+                a.partLen = (uint32_t)((tot / 64u + RT_COUNTER_PARTS - 1) / RT_COUNTER_PARTS * 64u);
+            }
             // such launches (a 1080p frame: ~400 work items per wave) refill at 16 free lanes, not 6:
             // 1080p 2-bounce frames -2.8 % (4K fused launches lose 5 % at 16,
             // profiles/r06/work_handout_ab.txt)
@@ -1281,8 +1301,8 @@ static int enqueue(rt_context ctx, rt_kernel k, size_t global_work_size, uint32_
     // (1080p: a 4-us fill and two ~6-us dispatch gaps in a ~0.28-ms frame)
     const bool pf_slots = RT_PF_COUNTER_SLOTS && !fused && si == RT_SCHED_STEP && !wf;
     if (pf_slots) {
-        a.workCounter = k->work_counter + 4 * (RT_RAD_SETS + k->pf_ctr);
-        a.workCounterClear = k->work_counter + 4 * (RT_RAD_SETS + (k->pf_ctr ^ 1));
+        a.workCounter = k->work_counter + 4 * RT_RAD_SETS + k->pf_ctr * rtk::kMaxParts * rtk::kPartStride;
+        a.workCounterClear = k->work_counter + 4 * RT_RAD_SETS + (k->pf_ctr ^ 1) * rtk::kMaxParts * rtk::kPartStride;
     } else if (si != RT_SCHED_TILES && !wf && clear_here) {
         hipError_t me = hipMemsetAsync(a.workCounter, 0, 16, rstr);
         if (me != hipSuccess) return map_hip(me);

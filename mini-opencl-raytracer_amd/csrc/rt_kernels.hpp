@@ -62,6 +62,9 @@ struct KernelArgs {
     uint32_t* workCounterClear;         // per-frame step launches: the other counter slot, zeroed by this launch
     uint32_t tailBase;                  // first tail work item the tail counter hands out (next_chunk)
     uint32_t staticFirst;               // step schedule: waves start with their own tail chunk (no bulk region)
+    // counter partitions (per-frame launches without a bulk region): nParts (a power of two) contiguous
+    // ranges of partLen work items, each with its tail counter at workCounter[kPartStride * q + 1]
+    uint32_t nParts, partLen;
 };
 
 constexpr int kSchedTiles = 0;  // one pixel per lane per 16x16 tile, all bounces in place
@@ -92,6 +95,9 @@ constexpr uint32_t kEndWalk = 0xff000000u;
 // LDS node records of trees with at most kOctBMaxStride records per plane keep their B planes at
 // the fixed float4 offset kOctB, so a node step reads B with an immediate offset from A's address
 constexpr uint32_t kOctBMaxStride = 64;
+// counter partitions: words between two partitions' counters (1 KB), and the most partitions
+constexpr uint32_t kPartStride = 256;
+constexpr uint32_t kMaxParts = 8;
 constexpr uint32_t kOctB = 8 * kOctBMaxStride;
 
 using KernelFn = void (*)(KernelArgs);

@@ -773,9 +773,50 @@ __device__ __forceinline__ float4 rad_load(const float4* p) {
 // Tail chunks come from a.tailBase on: the end of the bulk region, or -- per-frame launches whose
 // first chunks are handed out statically (a.staticFirst, rt_capi.cpp) -- past those chunks
 // (kFusedOnly: bodies for fused launches only, which never start statically: the bulk region's end).
+// Counter partitions (a.nParts > 1; per-frame launches without a bulk region, rt_capi.cpp): the work
+// items split into nParts contiguous ranges, each with its own tail counter on its own 1-KB line, so
+// the waves' grabs spread over nParts addresses instead of queueing on one; workgroup b's waves
+// belong to partition b % nParts and take chunks there, statically first, then from its counter,
+// then -- once it is dry -- from the other partitions' counters.  Partition q's range, the number of
+// waves it starts statically and the first work item its counter hands out:
+__device__ __forceinline__ void part_range(const KernelArgs& a, uint32_t q, uint32_t total, uint32_t& beg,
+                                           uint32_t& end, uint32_t& cbase) {
+    beg = min(q * a.partLen, total);
+    end = min(beg + a.partLen, total);
+    const uint32_t nw = gridDim.x > q ? 4u * ((gridDim.x - q + a.nParts - 1u) / a.nParts) : 0u;
+    cbase = min(beg + nw * a.tailChunk, end);
+}
+__device__ __forceinline__ bool next_chunk_parts(const KernelArgs& a, uint32_t total, uint32_t lane,
+                                                 uint32_t& base, uint32_t& len) {
+    const uint32_t p0 = blockIdx.x & (a.nParts - 1u);
+    for (uint32_t k = 0; k < a.nParts; ++k) {
+        const uint32_t q = (p0 + k) & (a.nParts - 1u);
+        uint32_t beg, end, cbase;
+        part_range(a, q, total, beg, end, cbase);
+        uint32_t* ctr = a.workCounter + kPartStride * q + 1u;
+        uint32_t b = 0;
+        if (k > 0) {
+            // another partition: skip it when its counter is already past its end (a plain read; a
+            // stale value is smaller, and only costs the atomic below)
+            if (lane == 0) b = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b = __shfl(b, 0, 64);
+            if (cbase + b >= end) continue;
+        }
+        if (lane == 0) b = atomicAdd(ctr, a.tailChunk);
+        b = __shfl(b, 0, 64) + cbase;
+        if (b < end) {
+            base = b;
+            len = min(a.tailChunk, end - b);
+            return true;
+        }
+    }
+    return false;
+}
+
 template <bool kFusedOnly>
 __device__ __forceinline__ bool next_chunk(const KernelArgs& a, uint32_t total, uint32_t lane, uint32_t& base,
                                            uint32_t& len, bool& tail) {
+    if (!kFusedOnly && a.nParts > 1u) return next_chunk_parts(a, total, lane, base, len);
     uint32_t b = 0;
     if (!tail) {
         if (lane == 0) b = atomicAdd(&a.workCounter[0], a.chunkPixels);
@@ -1006,8 +1047,14 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
             unsigned long long r = 0ull;
             if (!fused && a.staticFirst) {
                 const uint32_t tot = a.nTiles * 64u * (fused ? a.nFrames : 1u);
-                const uint32_t b0 = (blockIdx.x * 4u + (uint32_t)tid) * a.tailChunk;
-                if (b0 < tot) r = ((unsigned long long)min(b0 + a.tailChunk, tot) << 32) | b0;
+                uint32_t beg = 0, end = tot, wi = blockIdx.x * 4u + (uint32_t)tid;
+                if (a.nParts > 1u) {  // counter partitions: the wave's index among its partition's
+                    uint32_t cb;
+                    part_range(a, blockIdx.x & (a.nParts - 1u), tot, beg, end, cb);
+                    wi = (blockIdx.x / a.nParts) * 4u + (uint32_t)tid;
+                }
+                const uint32_t b0 = beg + wi * a.tailChunk;
+                if (b0 < end) r = ((unsigned long long)min(b0 + a.tailChunk, end) << 32) | b0;
             }
             steal[tid] = r;
         }
@@ -1015,7 +1062,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // per-frame launches alternate between two counter slots: this launch zeroes the one the next
     // launch takes (same stream, so that launch sees it) instead of a clearing launch in front of
     // each render (rt_capi.cpp)
-    if (!fused && a.workCounterClear && blockIdx.x == 0 && tid < 4) a.workCounterClear[tid] = 0u;
+    if (!fused && a.workCounterClear && blockIdx.x == 0 && (uint32_t)tid < 2u * max(a.nParts, 1u))
+        a.workCounterClear[kPartStride * ((uint32_t)tid >> 1) + ((uint32_t)tid & 1u)] = 0u;
     // the LDS walk on byte-address walk words (stage_scene_walk); kEndW the END word, rootW(sgn) the
     // root's word for a ray's octant
     constexpr bool kWalk = RT_WALK_ADDR && kLdsScene && !kGlobalOct;
