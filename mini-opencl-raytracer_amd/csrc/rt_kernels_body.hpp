@@ -1062,7 +1062,8 @@ __device__ __forceinline__ void step_body(const KernelArgs& a) {
     // per-frame launches alternate between two counter slots: this launch zeroes the one the next
     // launch takes (same stream, so that launch sees it) instead of a clearing launch in front of
     // each render (rt_capi.cpp)
-    if (!fused && a.workCounterClear && blockIdx.x == 0 && (uint32_t)tid < 2u * max(a.nParts, 1u))
+    // (every partition's words, whatever this launch uses: the next launch on that slot may use more)
+    if (!fused && a.workCounterClear && blockIdx.x == 0 && (uint32_t)tid < 2u * kMaxParts)
         a.workCounterClear[kPartStride * ((uint32_t)tid >> 1) + ((uint32_t)tid & 1u)] = 0u;
     // the LDS walk on byte-address walk words (stage_scene_walk); kEndW the END word, rootW(sgn) the
     // root's word for a ray's octant

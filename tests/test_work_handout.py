@@ -56,3 +56,27 @@ def test_per_frame_handout_bunny_proxy():
     from clrt import proxy
     sc = proxy.bunny_proxy()
     _same(_render(sc, 1920, 1080, 2, False), _render(sc, 1920, 1080, 2, True))
+
+
+def test_counter_slots_across_launch_sizes(cornell):
+    """Per-frame launches of different sizes on one kernel alternate between the two counter slots: a
+    partitioned 1080p launch (slot 0, 8 partitions), a small work-range launch (slot 1, one counter),
+    then the full frame again (slot 0).  Each launch zeroes every partition of the next slot, not just
+    the ones it uses, or the third launch would start from the first one's spent counters and skip
+    pixels.  Reference: the same sequence on the tile schedule (no counters)."""
+    W, H = 1920, 1080
+
+    def seq(sched):
+        r = HipRenderer(cornell, W, H, math=N.MATH_SHIPPED, hits=True, sched=sched)
+        r.ctx.WriteBuffer(r.hit_bufs[0], np.full(W * H, -2, np.int32))
+        if sched == N.SCHED_STEP:
+            r.k.set_tuning("perframe_defer", 0)
+        r.frame(1, light_bounces=2)
+        r.frame(2, light_bounces=2, work_range=(0, 64 * 1024))
+        r.k.set_work_range(0, 0)  # the whole frame again
+        r.frame(3, light_bounces=2)
+        out = (r.result(), r.hits())
+        r.close()
+        return out
+
+    _same(seq(N.SCHED_STEP), seq(N.SCHED_TILES))
