@@ -64,10 +64,6 @@ struct MathPinned {
     static constexpr int kId = 0;
     static constexpr bool kContract = false;
     // the reference's `/` and sqrt: IEEE, correctly rounded
-#if RT_PINNED_DIAG_DIV
-    __device__ __forceinline__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-    __device__ __forceinline__ static float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
-#else
     // 1.0f / x, correctly rounded, as the hardware reciprocal plus one Newton step (two fma): for
     // every float with an exponent field in [2, 251] this IS the IEEE quotient, bit for bit
     // (scripts/probes/pinned_fast_probe.hip, exhaustive: profiles/r06/pinned_fast_probe_v1.txt) --
@@ -77,6 +73,10 @@ struct MathPinned {
         const float y = __builtin_amdgcn_rcpf(x);
         return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
     }
+#if RT_PINNED_DIAG_DIV
+    __device__ __forceinline__ static float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+    __device__ __forceinline__ static float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+#else
     __device__ __forceinline__ static float rcp(float x) {
         const float r = rcp_fast(x);
         const bool ok = (__float_as_uint(x) & 0x7fffffffu) - 0x01000000u < 0x7d000000u;
